@@ -1,0 +1,240 @@
+"""oracle/oracle.py — TEST INFRASTRUCTURE ONLY (ctypes bindings for the oracles).
+
+Two CPU oracles live under oracle/ and are used only by tests/, bench.py's
+``cpu_baseline`` leg and ``__graft_entry__.smoke()`` as the *checker*:
+
+* ``RefLib``  — oracle/_ref/libpht_ref.so, the reference's own C
+  (/root/reference/src, compiled in place by oracle/Makefile against our
+  R-API shim).  ``gibbs`` is LJMA_Gibbs exactly as R's ``.C`` would call it.
+* ``OracleLib`` — oracle/_build/liboracle.so, our C restatement of the hot
+  path (pht_oracle.c).  ``ref`` variant: R-stream RNG + libm, bit-exact with
+  RefLib.  ``dev`` variant: Philox + detmath + fixed-point z, bit-exact with
+  the HIP kernels (the GPU specification).
+
+Nothing in phasetype_amd/ imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import glob
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF_SO = os.path.join(HERE, "_ref", "libpht_ref.so")
+ORC_SO = os.path.join(HERE, "_build", "liboracle.so")
+
+_dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_ip = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_lp = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+
+
+def lapack_path() -> tuple[str, str]:
+    """(path, symbol prefix) of an LP64 LAPACK: scipy's bundled OpenBLAS."""
+    env = os.environ.get("PHT_LAPACK_LIB")
+    if env:
+        return env, os.environ.get("PHT_LAPACK_PREFIX", "")
+    import scipy  # noqa: F401  (only to locate the wheel's .libs dir)
+
+    d = os.path.join(os.path.dirname(os.path.dirname(scipy.__file__)), "scipy.libs")
+    cands = sorted(glob.glob(os.path.join(d, "libscipy_openblas-*.so")))
+    if not cands:
+        raise RuntimeError("no LP64 LAPACK found (set PHT_LAPACK_LIB)")
+    return cands[0], "scipy_"
+
+
+def build(ref: bool = True) -> None:
+    targets = ["oracle"] + (["ref"] if ref else [])
+    subprocess.run(["make", "-s", "-C", HERE] + targets, check=True)
+
+
+def gibbs_argv(it, mhit, method, n, nu, zeta, T, C_, y, censored, start, silent):
+    """The 15 .C vectors of LJMA_Gibbs (src/PHT_MCMC_Aslett.c:104)."""
+    m = len(nu)
+    return dict(
+        it=np.array([it], np.int32), mhit=np.array([mhit], np.int32),
+        method=np.array([method], np.int32), n=np.array([n], np.int32),
+        m=np.array([m], np.int32), nu=np.ascontiguousarray(nu, np.float64),
+        zeta=np.ascontiguousarray(zeta, np.float64),
+        T=np.ascontiguousarray(np.asarray(T).reshape(-1, order="F") if np.ndim(T) == 2 else T, np.int32),
+        C=np.ascontiguousarray(np.asarray(C_).reshape(-1, order="F") if np.ndim(C_) == 2 else C_, np.float64),
+        y=np.ascontiguousarray(y, np.float64), l=np.array([len(y)], np.int32),
+        censored=np.ascontiguousarray(censored, np.int32),
+        start=np.ascontiguousarray(start, np.float64), silent=np.array([silent], np.int32),
+        res=np.zeros(it * m, np.float64),
+    )
+
+
+class RefLib:
+    """The reference's C compiled in place (oracle/_ref/libpht_ref.so)."""
+
+    def __init__(self, path: str = REF_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.lib = L = C.CDLL(path)
+        L.rshim_bind_lapack.argtypes = [C.c_char_p, C.c_char_p]
+        p, pre = lapack_path()
+        if L.rshim_bind_lapack(p.encode(), pre.encode()) != 0:
+            raise RuntimeError("could not bind LAPACK for the reference oracle")
+        L.rshim_set_seed.argtypes = [C.c_uint32]
+        L.rshim_set_verbose.argtypes = [C.c_int]
+        L.rshim_print_count.restype = C.c_long
+        L.ref_gibbs.argtypes = [_ip, _ip, _ip, _ip, _ip, _dp, _dp, _ip, _dp, _dp, _ip, _ip, _dp, _ip, _dp]
+        L.ref_eigen.argtypes = [C.c_int, _dp, _dp, _dp, _dp]
+        L.ref_sweep.argtypes = [C.c_int, C.c_int, _dp, _dp, C.c_int, _dp, _ip, C.c_int, C.c_int, _dp, _ip, _ip]
+        L.rshim_get_state.argtypes = [np.ctypeslib.ndpointer(dtype=np.uint32), C.POINTER(C.c_int)]
+
+    def set_seed(self, seed: int) -> None:
+        self.lib.rshim_set_seed(seed & 0xFFFFFFFF)
+
+    def gibbs(self, it, mhit, method, n, nu, zeta, T, C_, y, censored=None, start=None, silent=1):
+        if censored is None:
+            censored = np.zeros(len(y), np.int32)
+        if start is None:
+            start = np.array([-1.0])
+        a = gibbs_argv(it, mhit, method, n, nu, zeta, T, C_, y, censored, start, silent)
+        self.lib.ref_gibbs(*a.values())
+        return a["res"].reshape(len(nu), it).T.copy()  # res[iter + i*it]
+
+    def eigen(self, S):
+        n = S.shape[0]
+        ev = np.zeros(n)
+        Q = np.zeros(n * n)
+        Qi = np.zeros(n * n)
+        info = self.lib.ref_eigen(n, np.ascontiguousarray(S.reshape(-1, order="F")), ev, Q, Qi)
+        return info, ev, Q.reshape(n, n, order="F"), Qi.reshape(n, n, order="F")
+
+    def sweep(self, method, S, s, y, censored=None, mhit=1, per_obs=True):
+        n = S.shape[0]
+        y = np.ascontiguousarray(y, np.float64)
+        l = len(y)
+        cen = np.zeros(l, np.int32) if censored is None else np.ascontiguousarray(censored, np.int32)
+        k = l if per_obs else 1
+        z = np.zeros(k * n)
+        B = np.zeros(k if per_obs else n, np.int32)
+        N = np.zeros(k * n * n, np.int32)
+        self.lib.ref_sweep(method, n, np.ascontiguousarray(S.reshape(-1, order="F")), np.ascontiguousarray(s, np.float64),
+                           mhit, y, cen, l, int(per_obs), z, B, N)
+        if per_obs:
+            return B, z.reshape(l, n), N.reshape(l, n, n).transpose(0, 2, 1)  # N[obs, from, to]
+        return B, z, N.reshape(n, n).T
+
+    def state(self):
+        mt = np.zeros(624, np.uint32)
+        mti = C.c_int()
+        self.lib.rshim_get_state(mt, C.byref(mti))
+        return mt, mti.value
+
+
+_u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+
+
+def _opt(ptype):
+    """ndpointer that also accepts None (NULL)."""
+    class _P(ptype):
+        @classmethod
+        def from_param(cls, obj):
+            if obj is None:
+                return None
+            return ptype.from_param(obj)
+    return _P
+
+
+class OracleLib:
+    """Our CPU restatement (oracle/_build/liboracle.so)."""
+
+    def __init__(self, path: str = ORC_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.lib = L = C.CDLL(path)
+        L.orc_bind_lapack.argtypes = [C.c_char_p, C.c_char_p]
+        p, pre = lapack_path()
+        if L.orc_bind_lapack(p.encode(), pre.encode()) != 0:
+            raise RuntimeError("could not bind LAPACK for the oracle")
+        L.orc_set_seed.argtypes = [C.c_uint32]
+        L.orc_unif_rand.restype = C.c_double
+        L.orc_rgamma.restype = C.c_double
+        L.orc_rgamma.argtypes = [C.c_double, C.c_double]
+        L.orc_exp_rand.restype = C.c_double
+        L.orc_norm_rand.restype = C.c_double
+        L.orc_sp_size.restype = C.c_size_t
+        self.maxn = L.orc_maxn()
+        self.spsize = L.orc_sp_size()
+        L.orc_sp_build.argtypes = [C.c_void_p, C.c_int, _dp, _dp, C.c_int]
+        od, oi, ol, ou = _opt(_dp), _opt(_ip), _opt(_lp), _opt(_u32p)
+        ostats = _opt(_lp)
+        L.orc_ref_sweep.argtypes = [C.c_void_p, C.c_int, C.c_int, _dp, _ip, C.c_long, _dp, _ip, _ip,
+                                    oi, oi, od, oi, oi, ostats]
+        L.orc_dev_sweep.argtypes = [C.c_void_p, C.c_int, C.c_int, _dp, _ip, C.c_long, C.c_long,
+                                    C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, _lp, _lp, _lp,
+                                    oi, oi, od, ol, oi, oi, ou, ostats]
+        L.orc_zexp.argtypes = [_dp, C.c_long]
+        L.orc_gibbs.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _dp,
+                                _dp, C.c_long, _ip, _dp, _dp]
+
+    def set_seed(self, seed: int) -> None:
+        self.lib.orc_set_seed(seed & 0xFFFFFFFF)
+
+    def sp(self, S, s, method):
+        buf = C.create_string_buffer(self.spsize)
+        S = np.asarray(S, np.float64)
+        info = self.lib.orc_sp_build(buf, S.shape[0], np.ascontiguousarray(S.reshape(-1, order="F")),
+                                     np.ascontiguousarray(s, np.float64), method)
+        return buf, info
+
+    def ref_sweep(self, method, S, s, y, censored=None, mhit=1, per_obs=True):
+        n = S.shape[0]
+        y = np.ascontiguousarray(y, np.float64)
+        l = len(y)
+        cen = np.zeros(l, np.int32) if censored is None else np.ascontiguousarray(censored, np.int32)
+        sp, _ = self.sp(S, s, method)
+        zt, Bt, Nt = np.zeros(n), np.zeros(n, np.int32), np.zeros(n * n, np.int32)
+        if per_obs:
+            B, pre, z = np.zeros(l, np.int32), np.zeros(l, np.int32), np.zeros(l * n)
+            N, fl = np.zeros(l * n * n, np.int32), np.zeros(l, np.int32)
+        else:
+            B = pre = z = N = fl = None
+        stats = np.zeros(4, np.int64)
+        self.lib.orc_ref_sweep(sp, method, mhit, y, cen, l, zt, Bt, Nt, B, pre, z, N, fl, stats)
+        out = dict(z_tot=zt, B_tot=Bt, N_tot=Nt.reshape(n, n).T, stats=stats)
+        if per_obs:
+            out.update(B=B, pre=pre, z=z.reshape(l, n), N=N.reshape(l, n, n).transpose(0, 2, 1), flags=fl)
+        return out
+
+    def dev_sweep(self, method, S, s, y, censored=None, mhit=1, key=(1, 2), sweep=1, zexp=None,
+                  obs0=0, per_obs=True):
+        n = S.shape[0]
+        y = np.ascontiguousarray(y, np.float64)
+        l = len(y)
+        cen = np.zeros(l, np.int32) if censored is None else np.ascontiguousarray(censored, np.int32)
+        if zexp is None:
+            zexp = self.lib.orc_zexp(y, l)
+        sp, _ = self.sp(S, s, method)
+        zq, Bt, Nt = np.zeros(n, np.int64), np.zeros(n, np.int64), np.zeros(n * n, np.int64)
+        if per_obs:
+            B, pre, z = np.zeros(l, np.int32), np.zeros(l, np.int32), np.zeros(l * n)
+            zqo, N = np.zeros(l * n, np.int64), np.zeros(l * n * n, np.int32)
+            fl, nd = np.zeros(l, np.int32), np.zeros(l, np.uint32)
+        else:
+            B = pre = z = zqo = N = fl = nd = None
+        stats = np.zeros(4, np.int64)
+        self.lib.orc_dev_sweep(sp, method, mhit, y, cen, l, obs0, key[0], key[1], sweep, zexp, zq, Bt, Nt,
+                               B, pre, z, zqo, N, fl, nd, stats)
+        out = dict(zq_tot=zq, B_tot=Bt, N_tot=Nt.reshape(n, n).T, zexp=zexp, stats=stats)
+        if per_obs:
+            out.update(B=B, pre=pre, z=z.reshape(l, n), zq=zqo.reshape(l, n),
+                       N=N.reshape(l, n, n).transpose(0, 2, 1), flags=fl, ndraw=nd)
+        return out
+
+    def gibbs(self, dev, it, mhit, method, n, nu, zeta, T, C_, y, censored=None, start=None):
+        if censored is None:
+            censored = np.zeros(len(y), np.int32)
+        if start is None:
+            start = np.array([-1.0])
+        a = gibbs_argv(it, mhit, method, n, nu, zeta, T, C_, y, censored, start, 1)
+        self.lib.orc_gibbs(int(dev), it, mhit, method, n, len(nu), a["nu"], a["zeta"], a["T"], a["C"], a["y"],
+                           len(y), a["censored"], a["start"], a["res"])
+        return a["res"].reshape(len(nu), it).T.copy()

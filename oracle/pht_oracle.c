@@ -1,0 +1,371 @@
+/*
+ * oracle/pht_oracle.c — TEST INFRASTRUCTURE ONLY (never linked into the
+ * product; used by tests/, bench.py's cpu_baseline and smoke()).
+ *
+ * CPU restatement of the PhaseType Gibbs hot path:
+ *   - orc_sp_build: per-sweep embedded-chain and spectral data
+ *     (src/PHT_MCMC_Aslett.c:279-297,320-333; src/utility.c:50-129)
+ *   - orc_{ref,dev}_sweep: Gibbs step 1 over all observations
+ *     (src/PHT_MCMC_Aslett.c:325-337 and the samplers; see pht_oracle_impl.h)
+ *   - orc_{ref,dev}_gibbs: the full LJMA_Gibbs (src/PHT_MCMC_Aslett.c:104-410)
+ * "ref" = R-stream/libm/reference order (bit-exact with oracle/_ref);
+ * "dev" = the GPU specification (bit-exact with the HIP kernels).
+ */
+#include <dlfcn.h>
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "pht_detmath.h"
+#include "pht_philox.h"
+#include "../phasetype_amd/csrc/rstream.h"
+#include "pht_oracle.h"
+
+/* the host R stream of both variants (R's global RNG) */
+static pht_rstream g_rs;
+void orc_set_seed(uint32_t seed) { pht_rs_set_seed(&g_rs, seed); }
+double orc_unif_rand(void) { return pht_rs_unif_rand(&g_rs); }
+double orc_rgamma(double a, double scale) { return pht_rs_rgamma(&g_rs, a, scale); }
+double orc_exp_rand(void) { return pht_rs_exp_rand(&g_rs); }
+double orc_norm_rand(void) { return pht_rs_norm_rand(&g_rs); }
+
+/* ------------------------------------------------------------ variants */
+#define ORC_DEV 0
+#define ORC_FN(x) orcR_##x
+#include "pht_oracle_impl.h"
+#undef ORC_DEV
+#undef ORC_FN
+#undef ORC_EXP
+#undef ORC_LOG
+#define ORC_DEV 1
+#define ORC_FN(x) orcD_##x
+#include "pht_oracle_impl.h"
+#undef ORC_DEV
+#undef ORC_FN
+
+/* ------------------------------------------------------------- LAPACK */
+typedef void (*dgeevx_t)(const char *, const char *, const char *, const char *, const int *, double *,
+                         const int *, double *, double *, double *, const int *, double *, const int *,
+                         int *, int *, double *, double *, double *, double *, double *, const int *, int *,
+                         int *, size_t, size_t, size_t, size_t);
+typedef void (*dgetrf_t)(const int *, const int *, double *, const int *, int *, int *);
+typedef void (*dgetri_t)(const int *, double *, const int *, const int *, double *, const int *, int *);
+static dgeevx_t p_dgeevx;
+static dgetrf_t p_dgetrf;
+static dgetri_t p_dgetri;
+
+int orc_bind_lapack(const char *path, const char *prefix) {
+  void *h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) return 1;
+  char nm[64];
+  snprintf(nm, sizeof nm, "%sdgeevx_", prefix); p_dgeevx = (dgeevx_t)dlsym(h, nm);
+  snprintf(nm, sizeof nm, "%sdgetrf_", prefix); p_dgetrf = (dgetrf_t)dlsym(h, nm);
+  snprintf(nm, sizeof nm, "%sdgetri_", prefix); p_dgetri = (dgetri_t)dlsym(h, nm);
+  return (p_dgeevx && p_dgetrf && p_dgetri) ? 0 : 2;
+}
+
+/* LJMA_eigen with the LAPACK workspace sized as LJMA_Gibbs sizes it
+ * (src/PHT_MCMC_Aslett.c:177-185, src/utility.c:87-129). */
+static int orc_eigen(int n, const double *S, double *evals, double *Q, double *Qinv) {
+  if (!p_dgeevx) { fprintf(stderr, "oracle: LAPACK not bound\n"); abort(); }
+  char balanc = 'B', jobv = 'V', sense = 'B';
+  int lwork = -1, info, ilo, ihi, nn = n;
+  double wq, abnrm;
+  double A[ORC_MAXN * ORC_MAXN], evi[ORC_MAXN], Ql[ORC_MAXN * ORC_MAXN], scl[ORC_MAXN], rce[ORC_MAXN],
+      rcv[ORC_MAXN];
+  int iwork[4 * ORC_MAXN], ipiv[ORC_MAXN];
+  p_dgeevx(&balanc, &jobv, &jobv, &sense, &nn, A, &nn, evals, evi, Ql, &nn, Q, &nn, &ilo, &ihi, scl, &abnrm,
+           rce, rcv, &wq, &lwork, NULL, &info, 1, 1, 1, 1);
+  int lw = (int)wq;
+  p_dgetri(&nn, NULL, &nn, NULL, &wq, &lwork, &info);
+  if ((int)wq > lw) lw = (int)wq;
+  double *work = (double *)malloc(sizeof(double) * (lw > 0 ? lw : 1));
+  memcpy(A, S, sizeof(double) * n * n);
+  p_dgeevx(&balanc, &jobv, &jobv, &sense, &nn, A, &nn, evals, evi, Ql, &nn, Q, &nn, &ilo, &ihi, scl, &abnrm,
+           rce, rcv, work, &lw, iwork, &info, 1, 1, 1, 1);
+  if (info != 0) { free(work); return info; }
+  memcpy(Qinv, Q, sizeof(double) * n * n);
+  p_dgetrf(&nn, &nn, Qinv, &nn, ipiv, &info);
+  if (info == 0) p_dgetri(&nn, Qinv, &nn, ipiv, work, &lw, &info);
+  free(work);
+  return info;
+}
+
+/* Per-sweep data (src/PHT_MCMC_Aslett.c:279-297, :320-332) + device-mode
+ * precomputed products. */
+int orc_sp_build(orc_sp *sp, int n, const double *S, const double *s, int method) {
+  memset(sp, 0, sizeof *sp);
+  sp->n = n;
+  memcpy(sp->S, S, sizeof(double) * n * n);
+  memcpy(sp->s, s, sizeof(double) * n);
+  sp->pi[0] = 1.0; /* pi = e_1 (src/PHT_MCMC_Aslett.c:190-193) */
+  double *P = sp->P, *Pf = sp->Pfull;
+  for (int i = 0; i < n; i++) {
+    double rsum, rsumfull = 0.0;
+    for (int j = 0; j < n; j++) rsumfull += Pf[i + j * n] = P[i + j * n] = -S[i + j * n] / S[i + i * n];
+    rsum = rsumfull - P[i + i * n];
+    rsumfull += Pf[i + n * n] = -s[i] / S[i + i * n];
+    rsumfull -= Pf[i + i * n];
+    Pf[i + i * n] = P[i + i * n] = 0.0;
+    for (int j = 0; j < n; j++) {
+      P[i + j * n] = P[i + j * n] / rsum;
+      Pf[i + j * n] = Pf[i + j * n] / rsumfull;
+    }
+    Pf[i + n * n] = Pf[i + n * n] / rsumfull;
+  }
+  if (method & (ORC_ECS | ORC_DCS)) {
+    sp->eig_info = orc_eigen(n, S, sp->evals, sp->Q, sp->Qinv);
+    double one[ORC_MAXN];
+    for (int i = 0; i < n; i++) one[i] = 1.0;
+    orcR_gemv_n(n, sp->Qinv, s, sp->Qinv_s);
+    orcR_gemv_n(n, sp->Qinv, one, sp->Qinv_1);
+  }
+  /* device-mode products */
+  for (int j = 0; j < n; j++) {
+    const double Sjj = S[j + j * n];
+    sp->logs[j] = s[j] > 0.0 ? pht_log(s[j]) : 0.0;
+    sp->scale[j] = 1.0 / -Sjj;
+    sp->logscale[j] = pht_log(sp->scale[j]);
+    for (int i = 0; i < n; i++) {
+      double w = 0.0, v = 0.0;
+      for (int k = 0; k < n; k++) {
+        if (k != j) w = fma(S[j + k * n] / (-Sjj), sp->Q[k + i * n], w);
+        v = fma(P[j + k * n], sp->Q[k + i * n], v);
+      }
+      sp->QQs[j + i * n] = sp->Q[j + i * n] * sp->Qinv_s[i];
+      sp->W[j + i * n] = w * sp->Qinv_s[i];
+      sp->QQ1[j + i * n] = sp->Q[j + i * n] * sp->Qinv_1[i];
+      sp->V[j + i * n] = v * sp->Qinv_1[i];
+    }
+  }
+  for (int i = 0; i < n; i++) {
+    double a = 0.0;
+    for (int k = 0; k < n; k++) a = fma(sp->pi[k], sp->Q[k + i * n], a);
+    sp->piQ[i] = a;
+  }
+  return sp->eig_info;
+}
+
+size_t orc_sp_size(void) { return sizeof(orc_sp); }
+int orc_maxn(void) { return ORC_MAXN; }
+
+/* Copy one observation's result into flat per-observation arrays. */
+static void put_obs(const orc_obs *o, int n, long i, int *B, int *pre, double *z, int64_t *zq, int *N, int *flags,
+                    uint32_t *ndraw) {
+  if (B) B[i] = o->B;
+  if (pre) pre[i] = o->pre;
+  if (flags) flags[i] = o->flags;
+  if (ndraw) ndraw[i] = o->ndraw;
+  for (int k = 0; k < n; k++) {
+    if (z) z[i * n + k] = o->z[k];
+    if (zq) zq[i * n + k] = o->zq[k];
+  }
+  if (N) memcpy(N + i * n * n, o->N, sizeof(int) * n * n);
+}
+
+static int dispatch(int method) {
+  if (method & ORC_MHRS) return ORC_MHRS;
+  if (method & ORC_DCS) return ORC_DCS;
+  if (method & ORC_ECS) return ORC_ECS;
+  return 0;
+}
+
+/*
+ * Reference-variant step 1: observations in order on the global R stream.
+ * Totals: z_tot[n] (f64, summed per observation as the reference), B_tot[n],
+ * N_tot[n*n].  Per-observation arrays may be NULL.  stats[0..3] += jumps-ish
+ * counters (ARMS density evaluations, Brent evaluations).
+ */
+void orc_ref_sweep(const orc_sp *sp, int method, int mhit, const double *y, const int *cens, long l,
+                   double *z_tot, int *B_tot, int *N_tot, int *B, int *pre, double *z, int *N, int *flags,
+                   long *stats) {
+  const int n = sp->n;
+  int m = dispatch(method);
+  orc_obs o;
+  int neval = 0, nbrent = 0;
+  for (int k = 0; k < n; k++) { z_tot[k] = 0.0; B_tot[k] = 0; }
+  for (int k = 0; k < n * n; k++) N_tot[k] = 0;
+  for (long i = 0; i < l; i++) {
+    if (m == ORC_MHRS) orcR_obs_mhrs(sp, y[i], cens[i], mhit, &g_rs, &o, 0.0);
+    else if (m == ORC_DCS) orcR_obs_dcs(sp, y[i], &g_rs, &o, 0.0, &nbrent);
+    else if (cens[i]) orcR_obs_censored(sp, y[i], cens[i], &g_rs, &o, 0.0, &neval);
+    else orcR_obs_ecs_exact(sp, y[i], &g_rs, &o, 0.0, &neval);
+    B_tot[o.B]++;
+    for (int k = 0; k < n; k++) z_tot[k] += o.z[k];
+    for (int k = 0; k < n * n; k++) N_tot[k] += o.N[k];
+    put_obs(&o, n, i, B, pre, z, NULL, N, flags, NULL);
+  }
+  if (stats) { stats[0] += neval; stats[1] += nbrent; }
+}
+
+/*
+ * Device-variant step 1 (the GPU specification): observation i draws from
+ * its own Philox stream (key k0,k1; counter obs=obs0+i, tag 0, sweep).
+ * z is reduced as int64 fixed point with quantum 2^-zexp (zq_tot), counts
+ * as int64.  obs0 is the global index of y[0] (sharding).
+ */
+void orc_dev_sweep(const orc_sp *sp, int method, int mhit, const double *y, const int *cens, long l, long obs0,
+                   uint32_t k0, uint32_t k1, uint32_t sweep, int zexp, int64_t *zq_tot, int64_t *B_tot,
+                   int64_t *N_tot, int *B, int *pre, double *z, int64_t *zq, int *N, int *flags, uint32_t *ndraw,
+                   long *stats) {
+  const int n = sp->n;
+  const double zscale = ldexp(1.0, zexp);
+  int m = dispatch(method);
+  orc_obs o;
+  int neval = 0, nbrent = 0;
+  for (int k = 0; k < n; k++) { zq_tot[k] = 0; B_tot[k] = 0; }
+  for (int k = 0; k < n * n; k++) N_tot[k] = 0;
+  for (long i = 0; i < l; i++) {
+    pht_stream r;
+    pht_stream_init(&r, k0, k1, (uint32_t)(obs0 + i), 0u, sweep);
+    if (m == ORC_MHRS) orcD_obs_mhrs(sp, y[i], cens[i], mhit, &r, &o, zscale);
+    else if (m == ORC_DCS) orcD_obs_dcs(sp, y[i], &r, &o, zscale, &nbrent);
+    else if (cens[i]) orcD_obs_censored(sp, y[i], cens[i], &r, &o, zscale, &neval);
+    else orcD_obs_ecs_exact(sp, y[i], &r, &o, zscale, &neval);
+    if (m != ORC_MHRS) o.ndraw = pht_stream_pos(&r);
+    B_tot[o.B]++;
+    for (int k = 0; k < n; k++) zq_tot[k] += o.zq[k];
+    for (int k = 0; k < n * n; k++) N_tot[k] += o.N[k];
+    put_obs(&o, n, i, B, pre, z, zq, N, flags, ndraw);
+  }
+  if (stats) { stats[0] += neval; stats[1] += nbrent; }
+}
+
+/* fixed-point exponent for z: 52 - ceil(log2(sum(y) + 1)) */
+int orc_zexp(const double *y, long l) {
+  double sy = 0.0;
+  for (long i = 0; i < l; i++) sy += y[i];
+  int e = (int)ceil(log2(sy + 1.0));
+  return 52 - e;
+}
+
+/* ---------------------------------------------------------- Gibbs driver */
+typedef struct { int i, j; double c; } ent;
+
+/*
+ * LJMA_Gibbs restated (src/PHT_MCMC_Aslett.c:104-410).  dev=0: the sampler
+ * step is orc_ref_sweep on the global R stream (bit-exact with the
+ * reference).  dev=1: the sampler step is orc_dev_sweep, keyed by two
+ * uniforms drawn from the R stream at entry (k = floor(u * 2^32)), exactly
+ * as the product's LJMA_Gibbs does.  The linked-list parameter maps are kept
+ * as arrays visited in the lists' (reverse-insertion) order, which fixes the
+ * floating summation order of zsum and of the diagonal refresh.
+ */
+void orc_gibbs(int dev, int it, int mhit, int method, int n, int m, const double *nu, const double *zeta,
+               const int *T, const double *C, const double *y, long l, const int *censored, const double *start,
+               double *res) {
+  const int n1 = n + 1;
+  uint32_t k0 = 0, k1 = 0;
+  int zexp = 0;
+  if (dev) {
+    k0 = (uint32_t)(pht_rs_unif_rand(&g_rs) * 4294967296.0);
+    k1 = (uint32_t)(pht_rs_unif_rand(&g_rs) * 4294967296.0);
+    zexp = orc_zexp(y, l);
+  }
+  double *TT = (double *)calloc((size_t)n1 * n1, sizeof(double));
+  double S[ORC_MAXN * ORC_MAXN], s[ORC_MAXN];
+  /* per-parameter lists, insertion order (visited in reverse) */
+  ent **Nl = (ent **)calloc(m, sizeof(ent *)), **Sl = (ent **)calloc(m, sizeof(ent *)),
+      **sl = (ent **)calloc(m, sizeof(ent *)), **zl = (ent **)calloc(m, sizeof(ent *)),
+      **TTl = (ent **)calloc(m, sizeof(ent *)), **Dl = (ent **)calloc(n1, sizeof(ent *));
+  int *nN = calloc(m, sizeof(int)), *nS = calloc(m, sizeof(int)), *ns = calloc(m, sizeof(int)),
+      *nz = calloc(m, sizeof(int)), *nTT = calloc(m, sizeof(int)), *nD = calloc(n1, sizeof(int));
+  for (int k = 0; k < m; k++) {
+    size_t cap = (size_t)n1 * n1;
+    Nl[k] = malloc(cap * sizeof(ent)); Sl[k] = malloc(cap * sizeof(ent)); sl[k] = malloc(cap * sizeof(ent));
+    zl[k] = malloc(cap * sizeof(ent)); TTl[k] = malloc(cap * sizeof(ent));
+  }
+  for (int i = 0; i < n1; i++) Dl[i] = malloc((size_t)n1 * sizeof(ent));
+
+  if (start[0] < 0) {
+    for (int i = 0; i < m; i++)
+      res[0 + (size_t)i * it] = (nu[i] > 1) ? (nu[i] - 1.0) / zeta[i] : pht_rs_rgamma(&g_rs, nu[i], 1.0 / zeta[i]);
+  } else {
+    for (int i = 0; i < m; i++) res[0 + (size_t)i * it] = start[i];
+  }
+  double rsum = 0.0;
+  for (int i = 0; i < n1; i++) {
+    for (int j = 0; j < n1; j++) {
+      int t = T[i + j * n1];
+      if (t == 0) { TT[i + j * n1] = 0.0; continue; }
+      int k = t - 1;
+      double c = C[i + j * n1];
+      rsum -= TT[i + j * n1] = res[0 + (size_t)k * it] * c;
+      if (j == n) {
+        Nl[k][nN[k]++] = (ent){i, i, 1.0};
+        sl[k][ns[k]++] = (ent){i, 0, c};
+      } else {
+        Nl[k][nN[k]++] = (ent){i, j, 1.0};
+        Sl[k][nS[k]++] = (ent){i, j, c};
+      }
+      zl[k][nz[k]++] = (ent){i, 0, c};
+      TTl[k][nTT[k]++] = (ent){i, j, c};
+      Dl[i][nD[i]++] = (ent){i, j, 1.0};
+    }
+    TT[i + i * n1] = rsum;
+    rsum = 0.0;
+  }
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < n; j++) S[i + j * n] = TT[i + j * n1];
+  for (int i = 0; i < n; i++) s[i] = TT[i + n * n1];
+
+  orc_sp *sp = (orc_sp *)malloc(sizeof(orc_sp));
+  double z[ORC_MAXN];
+  int Bt[ORC_MAXN], Nt[ORC_MAXN * ORC_MAXN];
+  int64_t zq[ORC_MAXN], Bq[ORC_MAXN], Nq[ORC_MAXN * ORC_MAXN];
+  int *Nsum = calloc(m, sizeof(int));
+  double *zsum = calloc(m, sizeof(double));
+  int disp = dispatch(method);
+  for (int iter = 1; iter < it; iter++) {
+    if (!disp) continue; /* "CRITICAL ERROR: Unknown sampling method" */
+    orc_sp_build(sp, n, S, s, disp == ORC_MHRS ? ORC_MHRS : method);
+    if (!dev) {
+      orc_ref_sweep(sp, method, mhit, y, censored, l, z, Bt, Nt, NULL, NULL, NULL, NULL, NULL, NULL);
+    } else {
+      orc_dev_sweep(sp, method, mhit, y, censored, l, 0, k0, k1, (uint32_t)iter, zexp, zq, Bq, Nq, NULL, NULL,
+                    NULL, NULL, NULL, NULL, NULL, NULL);
+      for (int k = 0; k < n; k++) z[k] = ldexp((double)zq[k], -zexp);
+      for (int k = 0; k < n * n; k++) Nt[k] = (int)Nq[k];
+    }
+    for (int k = 0; k < m; k++) {
+      Nsum[k] = 0;
+      zsum[k] = 0.0;
+      for (int e = nN[k] - 1; e >= 0; e--) Nsum[k] += Nt[Nl[k][e].i + Nl[k][e].j * n];
+      for (int e = nz[k] - 1; e >= 0; e--) zsum[k] += z[zl[k][e].i] / zl[k][e].c;
+    }
+    for (int k = 0; k < m; k++) {
+      double tmp = res[iter + (size_t)k * it] = pht_rs_rgamma(&g_rs, nu[k] + Nsum[k], 1.0 / (zeta[k] + zsum[k]));
+      for (int e = nTT[k] - 1; e >= 0; e--) TT[TTl[k][e].i + TTl[k][e].j * n1] = tmp * TTl[k][e].c;
+      for (int e = nS[k] - 1; e >= 0; e--) S[Sl[k][e].i + Sl[k][e].j * n] = tmp * Sl[k][e].c;
+      for (int e = ns[k] - 1; e >= 0; e--) s[sl[k][e].i] = tmp * sl[k][e].c;
+    }
+    for (int i = 0; i < n; i++) {
+      double tmp = 0.0;
+      for (int e = nD[i] - 1; e >= 0; e--) tmp -= TT[Dl[i][e].i + Dl[i][e].j * n1];
+      TT[i + i * n1] = tmp;
+      S[i + i * n] = tmp;
+    }
+  }
+  free(sp); free(Nsum); free(zsum); free(TT);
+  for (int k = 0; k < m; k++) { free(Nl[k]); free(Sl[k]); free(sl[k]); free(zl[k]); free(TTl[k]); }
+  for (int i = 0; i < n1; i++) free(Dl[i]);
+  free(Nl); free(Sl); free(sl); free(zl); free(TTl); free(Dl);
+  free(nN); free(nS); free(ns); free(nz); free(nTT); free(nD);
+}
+
+/* primitive probes for tests/test_detmath.py and tests/test_philox.py */
+void orc_detexp_v(const double *x, double *y, long n) { for (long i = 0; i < n; i++) y[i] = pht_exp(x[i]); }
+void orc_detlog_v(const double *x, double *y, long n) { for (long i = 0; i < n; i++) y[i] = pht_log(x[i]); }
+void orc_philox(const uint32_t *ctr, uint32_t k0, uint32_t k1, uint32_t *out) {
+  pht_u32x4 c = {{ctr[0], ctr[1], ctr[2], ctr[3]}};
+  pht_u32x4 w = pht_philox4x32_10(c, k0, k1);
+  for (int i = 0; i < 4; i++) out[i] = w.v[i];
+}
+void orc_stream_u(uint32_t k0, uint32_t k1, uint32_t obs, uint32_t tag, uint32_t sweep, long cnt, double *out) {
+  pht_stream s;
+  pht_stream_init(&s, k0, k1, obs, tag, sweep);
+  for (long i = 0; i < cnt; i++) out[i] = pht_next_u(&s);
+}
