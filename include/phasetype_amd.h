@@ -1,0 +1,80 @@
+/*
+ * phasetype_amd.h — C ABI of the MI355X-native PhaseType hot path
+ * (libPhaseType.so, built by phasetype_amd/build.py).
+ *
+ * 1. Drop-in boundary (what R binds).  The reference registers exactly one
+ *    native routine, for `.C`:
+ *      src/PHT_MCMC_Aslett.h:1-3    void LJMA_Gibbs(int*, int*, int*, int*, int*, double*, double*,
+ *                                                   int*, double*, double*, int*, int*, double*, int*, double*)
+ *      src/Registrations.c:6-20     R_init_PhaseType: R_registerRoutines(.C, 15 typed args),
+ *                                   R_useDynamicSymbols(FALSE), R_forceSymbols(TRUE)
+ *      NAMESPACE:2                  useDynLib(PhaseType, .registration = TRUE)
+ *    Callers: R/phtMCMC.R:83, R/phtMCMC2.R:73.  Same names, same argument
+ *    meaning, same output layout (res[iter + i*it]); see INTEGRATION.md.
+ *
+ * 2. Sweep-level ABI (the seam the reference's LJMA_MHsample_{Bladt,
+ *    Aslett2,Hobolth2} occupy, src/PHT_MCMC_Aslett.c:325-333): one Gibbs
+ *    step 1 over a shard of observations on one GPU, returning the int64
+ *    sufficient-statistics block
+ *      [zq n][B n][N n*n][8 counters]   (pht_stats_len(n) entries)
+ *    zq = z in fixed point, z_k = zq_k * 2^-zexp; N[i + j n] = i->j
+ *    transitions, diagonal = absorb-from counts (reference convention).
+ *
+ * Errors: functions returning int return 0 on success and non-zero on
+ * failure with a message in pht_last_error().  There is no CPU fallback:
+ * without a HIP device, pht_ctx_create and LJMA_Gibbs fail loudly.
+ */
+#ifndef PHASETYPE_AMD_H
+#define PHASETYPE_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- drop-in boundary ------------------------------------------------ */
+void LJMA_Gibbs(int *it, int *mhit, int *method, int *n, int *m, double *nu, double *zeta, int *T, double *C,
+                double *y, int *l, int *censored, double *start, int *silent, double *res);
+void R_init_PhaseType(void *dll_info);
+
+/* ---- host services ----------------------------------------------------- */
+const char *pht_last_error(void);
+int pht_device_count(void);
+/* Bind an LP64 LAPACK (dgeevx_/dgetrf_/dgetri_ with symbol prefix); inside R
+ * the process's own LAPACK is found automatically. */
+int pht_bind_lapack(const char *path, const char *prefix);
+/* Standalone R-compatible random stream (ignored inside R): set.seed(seed). */
+void pht_set_seed(uint32_t seed);
+double pht_unif_rand(void);
+double pht_rgamma(double shape, double scale);
+int pht_in_R(void);
+void pht_set_verbose(int v);
+int pht_zexp(const double *y, long l);
+int pht_params_bytes(int n);
+int pht_stats_len(int n);
+int pht_build_params(int n, const double *S, const double *s, int method, unsigned char *out, int out_bytes);
+
+/* ---- sweep-level ABI ----------------------------------------------------- */
+typedef struct pht_ctx pht_ctx;
+pht_ctx *pht_ctx_create(int device, int n, int method, int mhit);
+void pht_ctx_destroy(pht_ctx *c);
+int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *censored, long count, long obs0);
+int pht_ctx_sweep(pht_ctx *c, const double *S, const double *s, uint32_t k0, uint32_t k1, uint32_t sweep,
+                  int zexp, long long *stats_out);
+int pht_ctx_sweep_debug(pht_ctx *c, const double *S, const double *s, uint32_t k0, uint32_t k1, uint32_t sweep,
+                        int zexp, long long *stats_out, int *B, int *pre, int *flags, uint32_t *ndraw,
+                        long long *zq, int *N);
+float pht_ctx_last_kernel_ms(pht_ctx *c);
+
+/* Gibbs loop over one shard; reduce(stats, len, user) must sum the int64
+ * block across all shards (return 0 on success). */
+typedef int (*pht_reduce_fn)(long long *stats, int len, void *user);
+int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double *nu, const double *zeta, const int *T,
+                  const double *C, int zexp, int silent, const double *start, double *res, pht_reduce_fn reduce,
+                  void *reduce_user, double *kernel_ms_total);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -146,6 +146,16 @@ int orc_sp_build(orc_sp *sp, int n, const double *S, const double *s, int method
     for (int k = 0; k < n; k++) a = fma(sp->pi[k], sp->Q[k + i * n], a);
     sp->piQ[i] = a;
   }
+  for (int j = 0; j < n; j++) {
+    int a = 0, b = 0, c = 0;
+    for (int k = 0; k < n; k++) {
+      if (!(P[j + k * n] == 0.0)) sp->succP[j * ORC_MAXN + a++] = k;
+      if (k != j && !(S[j + k * n] == 0.0)) sp->succS[j * ORC_MAXN + c++] = k;
+    }
+    for (int k = 0; k <= n; k++)
+      if (!(Pf[j + k * n] == 0.0)) sp->succPf[j * (ORC_MAXN + 1) + b++] = k;
+    sp->nsuccP[j] = a; sp->nsuccPf[j] = b; sp->nsuccS[j] = c;
+  }
   return sp->eig_info;
 }
 

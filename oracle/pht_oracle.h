@@ -32,6 +32,13 @@ typedef struct {
   double logs[ORC_MAXN];           /* log(s_j) (s_j > 0)                       */
   double scale[ORC_MAXN];          /* 1/-S_jj                                  */
   double logscale[ORC_MAXN];       /* log(1/-S_jj)                             */
+  /* candidate lists (device mode scans only these, in increasing index):
+   *   succP[j]  = {k : P[j,k] != 0}          (moveMass, censored jump)
+   *   succPf[j] = {k in 0..n : Pfull[j,k] != 0} (MHRS, censored t >= y)
+   *   succS[j]  = {i != j : S[j,i] != 0}     (DCS jump)                  */
+  int succP[ORC_MAXN * ORC_MAXN], nsuccP[ORC_MAXN];
+  int succPf[ORC_MAXN * (ORC_MAXN + 1)], nsuccPf[ORC_MAXN];
+  int succS[ORC_MAXN * ORC_MAXN], nsuccS[ORC_MAXN];
 } orc_sp;
 
 /* per-observation result */

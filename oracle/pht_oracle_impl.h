@@ -75,6 +75,14 @@ static void ORC_FN(obs_clear)(orc_obs *o, int n) {
   for (int i = 0; i < n * n; i++) o->N[i] = 0;
 }
 
+/* Device-mode termination caps: where the reference would loop forever or
+ * for an unbounded time (an ARMS envelope that rejects every proposal, a
+ * rejection sampler with vanishing acceptance), the device variant stops,
+ * sets a flag bit and carries on; the GPU must not hang a wave. */
+#define ORC_ARMS_MAXIT 10000      /* flag 4  */
+#define ORC_MAX_JUMPS (1 << 20)   /* flag 8  */
+#define ORC_MHRS_MAXATT (1 << 22) /* flag 16 */
+
 /* ------------------------------------------------------------- ARMS */
 #define ARMS_XEPS 0.00001
 #define ARMS_YEPS 0.1
@@ -242,7 +250,12 @@ static int ORC_FN(arms)(const double xinit[4], double xl, double xr, orc_dens f,
   e.xprev = xprev;
   e.yprev = f(xprev, ctx);
   e.neval++;
+#if ORC_DEV
+  for (int it = 0;; it++) {
+    if (it >= ORC_ARMS_MAXIT) { *xsamp = e.xprev; if (neval_out) *neval_out += e.neval; return 4; }
+#else
   for (;;) {
+#endif
     ORC_FN(wpt) p;
     ORC_FN(invert)(&e, ORC_FN(u)(rng), &p);
     /* test() (src/arms.c:424-521), metropolis on: no squeezing */
@@ -311,6 +324,32 @@ static inline int ORC_FN(catscan_s)(const double *w, int stride, int len, double
 static inline int ORC_FN(catscan)(const double *w, int len, double target, int *flags) {
   return ORC_FN(catscan_s)(w, 1, len, target, flags);
 }
+/* device mode: scan weights w[0..cnt) of candidates idx[0..cnt); running off
+ * the end (reference UB) selects the last candidate and flags it. */
+static inline int ORC_FN(catlist)(const double *w, const int *idx, int cnt, double target, int *flags) {
+  double sofar = 0.0;
+  for (int q = 0; q < cnt; q++) {
+    sofar += w[q];
+    if (!(sofar < target)) return idx[q];
+  }
+  *flags |= 1;
+  return cnt > 0 ? idx[cnt - 1] : 0;
+}
+/* start state ~ pi: "while(sofar < target) sofar += pi[B++]; B--" */
+static inline int ORC_FN(pistart)(const orc_sp *sp, double target, int *flags) {
+  double sofar = 0.0;
+  int B = 0;
+#if ORC_DEV
+  while (sofar < target) {
+    if (B >= sp->n) { *flags |= 1; return sp->n - 1; }
+    sofar += sp->pi[B++];
+  }
+#else
+  (void)flags;
+  while (sofar < target) sofar += sp->pi[B++];
+#endif
+  return B - 1;
+}
 
 /* ============================================================== MHRS */
 /*
@@ -322,10 +361,13 @@ static int ORC_FN(bladt_chain)(const orc_sp *sp, double y, int cens, ORC_FN(rng)
                                orc_obs *o, double zscale, int record, uint32_t *start_pos) {
   const int n = sp->n;
   double t = 0.0, lastt = 0.0;
-  int B2 = 0, lastj = 0, j;
+  int B2 = 0, lastj = 0, j, natt = 0;
   double z2[ORC_MAXN];
   int N2[ORC_MAXN * ORC_MAXN];
   while (t < y) {
+#if ORC_DEV
+    if (natt++ >= ORC_MHRS_MAXATT) { o->flags |= 16; break; }
+#endif
 #if ORC_DEV
     if (start_pos) *start_pos = pht_stream_pos(rng);
 #endif
@@ -339,13 +381,30 @@ static int ORC_FN(bladt_chain)(const orc_sp *sp, double y, int cens, ORC_FN(rng)
     j = B2;
     lastt = t;
     lastj = j;
+    int njump = 0;
     while ((t < y && j < n) || (cens && j < n)) {
+#if ORC_DEV
+      if (njump++ >= ORC_MAX_JUMPS) { o->flags |= 8; t = y; break; }
+#endif
       t = t + ORC_FN(rexp)(rng, 1.0 / -sp->S[j + j * n]);
       target = ORC_FN(u)(rng);
+#if ORC_DEV
+      {
+        const int *L = sp->succPf + j * (ORC_MAXN + 1);
+        int cnt = sp->nsuccPf[j], q = 0;
+        sofar = 0.0;
+        for (; q < cnt; q++) {
+          sofar += sp->Pfull[j + L[q] * n];
+          if (!(sofar < target)) break;
+        }
+        j = (q < cnt) ? L[q] : n + 1;
+      }
+#else
       int jj = 0;
       sofar = 0.0;
       while (sofar < target && jj <= n) sofar += sp->Pfull[j + jj * n], jj++;
       j = (sofar < target) ? n + 1 : jj - 1; /* scan past Pfull reads workspace: j=n+1 either way */
+#endif
       if ((t < y && j < n) || (cens && j < n)) {
         z2[lastj] += t - lastt;
         N2[lastj + j * n]++;
@@ -380,15 +439,22 @@ static void ORC_FN(bladt_replay)(const orc_sp *sp, double y, int cens, const ORC
   int B2 = 0;
   while (sofar < target && B2 <= n) sofar += sp->pi[B2++];
   B2--;
-  int j = B2, lastj = j;
+  int j = B2, lastj = j, njump = 0;
   o->B = B2;
   while ((t < y && j < n) || (cens && j < n)) {
+    if (njump++ >= ORC_MAX_JUMPS) { t = y; break; }
     t = t + ORC_FN(rexp)(&r, 1.0 / -sp->S[j + j * n]);
     target = ORC_FN(u)(&r);
-    int jj = 0;
-    sofar = 0.0;
-    while (sofar < target && jj <= n) sofar += sp->Pfull[j + jj * n], jj++;
-    j = (sofar < target) ? n + 1 : jj - 1;
+    {
+      const int *L = sp->succPf + j * (ORC_MAXN + 1);
+      int cnt = sp->nsuccPf[j], q = 0;
+      sofar = 0.0;
+      for (; q < cnt; q++) {
+        sofar += sp->Pfull[j + L[q] * n];
+        if (!(sofar < target)) break;
+      }
+      j = (q < cnt) ? L[q] : n + 1;
+    }
     if ((t < y && j < n) || (cens && j < n)) {
       ORC_FN(zadd)(o, lastj, t - lastt, zscale);
       o->N[lastj + j * n]++;
@@ -479,15 +545,16 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
                                   double zscale, int *neval) {
   const int n = sp->n;
   ORC_FN(obs_clear)(o, n);
-  double target = ORC_FN(u)(rng), sofar = 0.0;
-  int B = 0;
-  while (sofar < target) sofar += sp->pi[B++];
-  B--;
+  double target = ORC_FN(u)(rng);
+  int B = ORC_FN(pistart)(sp, target, &o->flags);
   o->B = B;
   double t = 0.0, d;
   int j = B, lastj;
   double p[ORC_MAXN + 1];
-  for (;;) {
+  for (int njump = 0;; njump++) {
+#if ORC_DEV
+    if (njump >= ORC_MAX_JUMPS) { o->flags |= 8; break; }
+#endif
     double y_t = y - t;
     if (sp->s[j] > 0.0) {
       double U = ORC_FN(u)(rng), pab;
@@ -514,23 +581,25 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
     xinit[2] = xinit[1] * 2.0;
     xinit[3] = y_t - xinit[0];
     double xsamp = 0.0;
-    ORC_FN(arms)(xinit, 0.0, y_t, ORC_FN(ecs_dens), &ctx, 0.0, &xsamp, rng, neval);
+    int ainfo = ORC_FN(arms)(xinit, 0.0, y_t, ORC_FN(ecs_dens), &ctx, 0.0, &xsamp, rng, neval);
+    if (ainfo) o->flags |= (ainfo == 4) ? 4 : 32;
     t += d = xsamp;
     /* LJMA_moveMass (:21-41) then the categorical draw (:352-358) */
     double x = y_t - d;
 #if ORC_DEV
     double E[ORC_MAXN], w[ORC_MAXN], sum = 0.0;
+    const int *L = sp->succP + j * ORC_MAXN;
+    const int cnt = sp->nsuccP[j];
     for (int i = 0; i < n; i++) E[i] = ORC_EXP(sp->evals[i] * x);
-    for (int k = 0; k < n; k++) {
-      double pk = sp->P[j + k * n];
-      if (pk == 0.0) { w[k] = 0.0; continue; }
+    for (int q = 0; q < cnt; q++) {
+      const int k = L[q];
       double acc = 0.0;
       for (int i = 0; i < n; i++) acc = fma(sp->QQs[k + i * n], E[i], acc);
-      w[k] = pk * acc;
-      sum += w[k];
+      w[q] = sp->P[j + k * n] * acc;
+      sum += w[q];
     }
     target = ORC_FN(u)(rng) * sum;
-    j = ORC_FN(catscan)(w, n, target, &o->flags);
+    j = ORC_FN(catlist)(w, L, cnt, target, &o->flags);
 #else
     double tmp[ORC_MAXN], pp[ORC_MAXN], sum = 0.0;
     for (int i = 0; i < n; i++) tmp[i] = ORC_EXP(sp->evals[i] * x) * sp->Qinv_s[i];
@@ -593,7 +662,7 @@ static double ORC_FN(cj_dens)(double d, void *vctx) {
 
 /* LJMA_condjump_r_ars (:184-260) */
 static double ORC_FN(condjump)(const orc_sp *sp, double tnow, int jnow, double y, ORC_FN(rng) *rng,
-                               int *neval) {
+                               int *neval, int *flags) {
   const int n = sp->n;
   if (tnow >= y) return ORC_FN(rexp)(rng, 1.0 / -sp->S[jnow + jnow * n]);
   double x = y - tnow, denom;
@@ -616,7 +685,8 @@ static double ORC_FN(condjump)(const orc_sp *sp, double tnow, int jnow, double y
   xinit[2] = xinit[1] * 2.0;
   xinit[3] = y - tnow - xinit[0];
   double xsamp = 0.0;
-  ORC_FN(arms)(xinit, 0.0, y - tnow, ORC_FN(cj_dens), &ctx, 0.0, &xsamp, rng, neval);
+  int ainfo = ORC_FN(arms)(xinit, 0.0, y - tnow, ORC_FN(cj_dens), &ctx, 0.0, &xsamp, rng, neval);
+  if (ainfo) *flags |= (ainfo == 4) ? 4 : 32;
   return xsamp;
 }
 
@@ -626,32 +696,35 @@ static void ORC_FN(obs_censored)(const orc_sp *sp, double y, int cens, ORC_FN(rn
   const int n = sp->n;
   ORC_FN(obs_clear)(o, n);
   double target = ORC_FN(u)(rng), sofar = 0.0;
-  int B = 0;
-  while (sofar < target) sofar += sp->pi[B++];
-  B--;
+  int B = ORC_FN(pistart)(sp, target, &o->flags);
   o->B = B;
   double t = 0.0, lastt = 0.0;
-  int j = B, lastj = 0;
+  int j = B, lastj = 0, njump = 0;
   while (t < y || cens) {
+#if ORC_DEV
+    if (njump++ >= ORC_MAX_JUMPS) { o->flags |= 8; break; }
+#endif
     lastt = t;
     lastj = j;
-    double d = ORC_FN(condjump)(sp, t, j, y, rng, neval);
+    double d = ORC_FN(condjump)(sp, t, j, y, rng, neval, &o->flags);
     t += d;
     target = ORC_FN(u)(rng);
     if (t < y) {
       double x1 = y - t;
 #if ORC_DEV
       double E[ORC_MAXN], w[ORC_MAXN], r2 = 0.0;
+      (void)sofar;
+      const int *L = sp->succP + lastj * ORC_MAXN;
+      const int cnt = sp->nsuccP[lastj];
       for (int i = 0; i < n; i++) E[i] = ORC_EXP(sp->evals[i] * x1);
       for (int i = 0; i < n; i++) r2 = fma(sp->V[lastj + i * n], E[i], r2);
-      for (int k = 0; k < n; k++) {
-        double pk = sp->P[lastj + k * n];
-        if (pk == 0.0) { w[k] = 0.0; continue; }
+      for (int q = 0; q < cnt; q++) {
+        const int k = L[q];
         double r1 = 0.0;
         for (int i = 0; i < n; i++) r1 = fma(sp->QQ1[k + i * n], E[i], r1);
-        w[k] = r1 * pk;
+        w[q] = r1 * sp->P[lastj + k * n];
       }
-      j = ORC_FN(catscan)(w, n, target * r2, &o->flags);
+      j = ORC_FN(catlist)(w, L, cnt, target * r2, &o->flags);
 #else
       double pi2[ORC_MAXN], pi1[ORC_MAXN];
       for (int i = 0; i < n; i++) pi2[i] = sp->P[lastj + i * n];
@@ -669,7 +742,17 @@ static void ORC_FN(obs_censored)(const orc_sp *sp, double y, int cens, ORC_FN(rn
       j--;
 #endif
     } else {
+#if ORC_DEV
+      {
+        const int *L = sp->succPf + lastj * (ORC_MAXN + 1);
+        const int cnt = sp->nsuccPf[lastj];
+        double w[ORC_MAXN + 1];
+        for (int q = 0; q < cnt; q++) w[q] = sp->Pfull[lastj + L[q] * n];
+        j = ORC_FN(catlist)(w, L, cnt, target, &o->flags);
+      }
+#else
       j = ORC_FN(catscan_s)(sp->Pfull + lastj, n, n + 1, target, &o->flags);
+#endif
     }
     if (j == n) break;
     if (t < y || cens) {
@@ -690,6 +773,7 @@ typedef struct {
   double prob, Pab, y, t, u;
   const double *Qb; /* Qinv e_b */
   double *J;
+  const double *E;  /* device mode: e^{lambda_i (y - t)} of this jump */
 } ORC_FN(hob_ctx);
 
 /* HobCDF (src/Simulate_AbsCTMC_gt_Hobolth_DCS.c:23-40) */
@@ -699,11 +783,15 @@ static double ORC_FN(hobcdf)(double x, void *vctx) {
   const int n = sp->n;
   const double Sll = sp->S[c->lastj + c->lastj * n];
   for (int i = 0; i < n; i++) {
+#if ORC_DEV
+    const double Ei = c->E[i];
+#else
+    const double Ei = ORC_EXP(sp->evals[i] * (c->y - c->t));
+#endif
     if (fabs((sp->evals[i] - Sll) / Sll) < 1e-13)
-      c->J[i] = x * ORC_EXP(sp->evals[i] * (c->y - c->t));
+      c->J[i] = x * Ei;
     else
-      c->J[i] = (ORC_EXP(sp->evals[i] * (c->y - c->t)) - ORC_EXP((c->y - c->t - x) * sp->evals[i] + Sll * x)) /
-                (sp->evals[i] - Sll);
+      c->J[i] = (Ei - ORC_EXP((c->y - c->t - x) * sp->evals[i] + Sll * x)) / (sp->evals[i] - Sll);
   }
   double tmp = 0.0;
 #if ORC_DEV
@@ -780,7 +868,9 @@ static void ORC_FN(obs_dcs)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_ob
     pend[k] = acc * sp->s[k];
     sum += pend[k];
   }
-  int b = ORC_FN(catscan)(pend, n, ORC_FN(u)(rng) * sum, &o->flags);
+  int allidx[ORC_MAXN];
+  for (int k = 0; k < n; k++) allidx[k] = k;
+  int b = ORC_FN(catlist)(pend, allidx, n, ORC_FN(u)(rng) * sum, &o->flags);
 #else
   double pq[ORC_MAXN], tmp[ORC_MAXN];
   ORC_FN(gemv_t)(n, sp->Q, sp->pi, pq);
@@ -798,14 +888,16 @@ static void ORC_FN(obs_dcs)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_ob
   ORC_FN(gemv_n)(n, sp->Qinv, bvec, Qb);
 #endif
   /* LJMA_samplechain_Hobolth */
-  double target = ORC_FN(u)(rng), sofar = 0.0;
-  int B = 0;
-  while (sofar < target) sofar += sp->pi[B++];
-  B--;
+  double target = ORC_FN(u)(rng);
+  int B = ORC_FN(pistart)(sp, target, &o->flags);
   o->B = B;
   double t = 0.0, jtime = 0.0, J[ORC_MAXN], p[ORC_MAXN];
-  int j = B, lastj;
+  (void)p;
+  int j = B, lastj, njump = 0;
   while (t < y) {
+#if ORC_DEV
+    if (njump++ >= ORC_MAX_JUMPS) { o->flags |= 8; break; }
+#endif
     lastj = j;
     double Pab = 0.0, x = y - t;
     (void)x;
@@ -834,24 +926,44 @@ static void ORC_FN(obs_dcs)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_ob
       else J[i] = (ORC_EXP(sp->evals[i] * (y - t)) - ORC_EXP(Sjj * (y - t))) / (sp->evals[i] - Sjj);
 #endif
     }
-    double p_sum = 0.0;
-    for (int i = 0; i < n; i++) {
-      if (i == j) continue;
+    double p_sum = 0.0, prob;
 #if ORC_DEV
-      if (sp->S[j + i * n] == 0.0) { p[i] = 0.0; continue; }
+    const int *L = sp->succS + j * ORC_MAXN;
+    const int cnt = sp->nsuccS[j];
+    double pw[ORC_MAXN];
+    for (int q = 0; q < cnt; q++) {
+      const int i = L[q];
       double tmp = 0.0;
       for (int k = 0; k < n; k++) tmp = fma(sp->Q[i + k * n] * J[k], Qb[k], tmp);
+      p_sum += pw[q] = sp->S[j + i * n] / Pab * tmp;
+    }
+    target = ORC_FN(runif)(rng, 0.0, p_sum);
+    if (!(target > 0.0)) { o->flags |= 2; o->pre = j; return; } /* reference reads p[-1]: UB */
+    {
+      double sofar = 0.0;
+      int q = 0;
+      for (; q < cnt; q++) { sofar += pw[q]; if (!(sofar < target)) break; }
+      if (q == cnt) { o->flags |= 1; q = cnt - 1; }
+      j = L[q];
+      prob = pw[q];
+    }
 #else
+    for (int i = 0; i < n; i++) {
+      if (i == j) continue;
       double tmp = 0.0;
       for (int k = 0; k < n; k++) tmp += sp->Q[i + k * n] * J[k] * Qb[k];
-#endif
       p_sum += p[i] = sp->S[j + i * n] / Pab * tmp;
     }
     p[j] = 0.0;
     target = ORC_FN(runif)(rng, 0.0, p_sum);
     if (!(target > 0.0)) { o->flags |= 2; o->pre = j; return; } /* reference reads p[-1]: UB */
     j = ORC_FN(catscan)(p, n, target, &o->flags);
-    ORC_FN(hob_ctx) hc = {sp, lastj, j, p[j], Pab, y, t, 0.0, Qb, J};
+    prob = p[j];
+#endif
+    ORC_FN(hob_ctx) hc = {sp, lastj, j, prob, Pab, y, t, 0.0, Qb, J, NULL};
+#if ORC_DEV
+    hc.E = E;
+#endif
     hc.u = ORC_FN(runif)(rng, 0.0, 1.0);
     double Tol = 0.0;
     int Maxit = 1000;

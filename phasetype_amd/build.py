@@ -1,0 +1,73 @@
+"""Build the native library in-tree: phasetype_amd/_lib/libPhaseType.so.
+
+One hipcc invocation for gfx950: HIP kernels (pht_kernels.hip), the host
+runtime / C ABI (gibbs_host.cpp) and the R-compatible stream (rstream.c).
+``-ffp-contract=off`` is required: the device path must reproduce the
+oracle's arithmetic bit for bit (no implicit FMA contraction anywhere).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT_DIR = os.path.join(HERE, "_lib")
+LIB = os.path.join(OUT_DIR, "libPhaseType.so")
+SOURCES = ["pht_kernels.hip", "gibbs_host.cpp", "rstream.c"]
+HEADERS = ["pht_device.h", "pht_env.h", "pht_kernels.h", "pht_layout.h", "rstream.h"]
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+
+
+def _hipcc() -> str:
+    for c in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps += [os.path.join(REPO, "include", f) for f in ("phasetype_amd.h", "pht_detmath.h", "pht_philox.h")]
+    deps.append(__file__)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return LIB
+    os.makedirs(OUT_DIR, exist_ok=True)
+    objs = []
+    for src in SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(OUT_DIR, src + ".o")
+        cmd = [_hipcc(), "-O3", "-fPIC", "-ffp-contract=off", f"-I{os.path.join(REPO, 'include')}", f"-I{CSRC}",
+               "-Wno-pass-failed"]
+        if src.endswith(".hip"):
+            cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-std=c++17"]
+        elif src.endswith(".cpp"):
+            cmd += ["-x", "c++", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
+        else:
+            cmd += ["-x", "c", "-std=gnu11"]
+        cmd += ["-c", path, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    tmp = LIB + ".tmp"
+    cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + ["-ldl"]
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

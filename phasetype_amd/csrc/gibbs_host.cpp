@@ -1,0 +1,780 @@
+/*
+ * gibbs_host.cpp — host runtime of the MI355X PhaseType hot path.
+ *
+ *  - LJMA_Gibbs: the reference's .C entry point (src/PHT_MCMC_Aslett.c:104,
+ *    registered by src/Registrations.c:6-20), re-implemented: the Gibbs
+ *    bookkeeping and conjugate Gamma update stay on the host exactly as in
+ *    src/PHT_MCMC_Aslett.c:187-405; step 1 (the per-observation latent-path
+ *    sampling, :276-337) runs as HIP kernels on every visible GPU, each GPU
+ *    owning a contiguous shard of the observations, and the integer
+ *    sufficient statistics are summed on the host (exact, order-free).
+ *  - R_init_PhaseType: registers LJMA_Gibbs for `.C` when loaded by R.
+ *  - pht_* : the sweep-level C ABI (include/phasetype_amd.h) used by the
+ *    Python mirror, the parity tests and the multi-process benchmark.
+ *
+ * Random numbers: inside R, R's own unif_rand/rgamma (resolved at run time);
+ * standalone, the R-compatible stream of rstream.c.  Per-observation draws
+ * on the device come from Philox keyed by two R-stream uniforms drawn at
+ * LJMA_Gibbs entry (pht_philox.h).
+ */
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/phasetype_amd.h"
+#include "pht_detmath.h"
+#include "pht_kernels.h"
+#include "pht_layout.h"
+#include "rstream.h"
+
+using namespace pht;
+
+/* ======================================================= error reporting */
+static thread_local std::string g_err;
+static void set_err(const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+extern "C" const char *pht_last_error(void) { return g_err.c_str(); }
+
+#define HIPCHK(x)                                                               \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      set_err("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return -1;                                                                \
+    }                                                                           \
+  } while (0)
+
+/* ================================================ R runtime (when inside R) */
+namespace {
+typedef double (*unif_fn)(void);
+typedef double (*rgamma_fn)(double, double);
+typedef void (*void_fn)(void);
+typedef void (*printf_fn)(const char *, ...);
+typedef void (*error_fn)(const char *, ...);
+
+struct RHost {
+  bool inR = false;
+  unif_fn unif = nullptr;
+  rgamma_fn rgamma = nullptr;
+  void_fn getrng = nullptr, putrng = nullptr, flush = nullptr;
+  printf_fn rprintf = nullptr;
+  error_fn rerror = nullptr;
+  pht_rstream rs;
+  bool seeded = false;
+  RHost() {
+    unif = (unif_fn)dlsym(RTLD_DEFAULT, "unif_rand");
+    rgamma = (rgamma_fn)dlsym(RTLD_DEFAULT, "rgamma");
+    getrng = (void_fn)dlsym(RTLD_DEFAULT, "GetRNGstate");
+    putrng = (void_fn)dlsym(RTLD_DEFAULT, "PutRNGstate");
+    rprintf = (printf_fn)dlsym(RTLD_DEFAULT, "Rprintf");
+    rerror = (error_fn)dlsym(RTLD_DEFAULT, "Rf_error");
+    flush = (void_fn)dlsym(RTLD_DEFAULT, "R_FlushConsole");
+    inR = unif && rgamma && getrng && putrng && rprintf && !getenv("PHT_STANDALONE_RNG");
+    pht_rs_set_seed(&rs, 1234u);
+  }
+  double u() { return inR ? unif() : pht_rs_unif_rand(&rs); }
+  double gamma(double a, double sc) { return inR ? rgamma(a, sc) : pht_rs_rgamma(&rs, a, sc); }
+  void begin() { if (inR) getrng(); }
+  void end() { if (inR) putrng(); }
+};
+RHost &rhost() {
+  static RHost h;
+  return h;
+}
+int g_verbose = 0;
+void say(const char *fmt, ...) {
+  RHost &h = rhost();
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (h.inR) {
+    h.rprintf("%s", buf);
+    if (h.flush) h.flush();
+  } else if (g_verbose) {
+    fputs(buf, stdout);
+    fflush(stdout);
+  }
+}
+}  // namespace
+
+extern "C" void pht_set_seed(uint32_t seed) { pht_rs_set_seed(&rhost().rs, seed); }
+extern "C" double pht_unif_rand(void) { return rhost().u(); }
+extern "C" double pht_rgamma(double a, double scale) { return rhost().gamma(a, scale); }
+extern "C" void pht_set_verbose(int v) { g_verbose = v; }
+extern "C" int pht_in_R(void) { return rhost().inR ? 1 : 0; }
+
+/* ================================================================ LAPACK */
+namespace {
+typedef void (*dgeevx_t)(const char *, const char *, const char *, const char *, const int *, double *,
+                         const int *, double *, double *, double *, const int *, double *, const int *, int *,
+                         int *, double *, double *, double *, double *, double *, const int *, int *, int *,
+                         size_t, size_t, size_t, size_t);
+typedef void (*dgetrf_t)(const int *, const int *, double *, const int *, int *, int *);
+typedef void (*dgetri_t)(const int *, double *, const int *, const int *, double *, const int *, int *);
+dgeevx_t p_dgeevx = nullptr;
+dgetrf_t p_dgetrf = nullptr;
+dgetri_t p_dgetri = nullptr;
+
+bool lapack_ready() {
+  if (p_dgeevx) return true;
+  /* inside R (or any process with an LP64 LAPACK loaded globally) */
+  p_dgeevx = (dgeevx_t)dlsym(RTLD_DEFAULT, "dgeevx_");
+  p_dgetrf = (dgetrf_t)dlsym(RTLD_DEFAULT, "dgetrf_");
+  p_dgetri = (dgetri_t)dlsym(RTLD_DEFAULT, "dgetri_");
+  if (p_dgeevx && p_dgetrf && p_dgetri) return true;
+  p_dgeevx = nullptr;
+  const char *path = getenv("PHT_LAPACK_LIB");
+  if (path) return pht_bind_lapack(path, getenv("PHT_LAPACK_PREFIX") ? getenv("PHT_LAPACK_PREFIX") : "") == 0;
+  return false;
+}
+}  // namespace
+
+extern "C" int pht_bind_lapack(const char *path, const char *prefix) {
+  void *h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    set_err("dlopen(%s): %s", path, dlerror());
+    return 1;
+  }
+  std::string pre = prefix ? prefix : "";
+  p_dgeevx = (dgeevx_t)dlsym(h, (pre + "dgeevx_").c_str());
+  p_dgetrf = (dgetrf_t)dlsym(h, (pre + "dgetrf_").c_str());
+  p_dgetri = (dgetri_t)dlsym(h, (pre + "dgetri_").c_str());
+  if (!(p_dgeevx && p_dgetrf && p_dgetri)) {
+    p_dgeevx = nullptr;
+    set_err("LAPACK symbols %sdgeevx_/dgetrf_/dgetri_ not found in %s", pre.c_str(), path);
+    return 2;
+  }
+  return 0;
+}
+
+/* LJMA_eigen with LJMA_Gibbs's workspace sizing (src/utility.c:87-129,
+ * src/PHT_MCMC_Aslett.c:177-185). */
+static int eigen(int n, const double *S, double *evals, double *Q, double *Qinv) {
+  char balanc = 'B', jobv = 'V', sense = 'B';
+  int lwork = -1, info = 0, ilo, ihi, nn = n;
+  double wq = 0, abnrm;
+  std::vector<double> A(n * n), evi(n), Ql(n * n), scl(n), rce(n), rcv(n);
+  std::vector<int> iwork(2 * n + 2), ipiv(n);
+  p_dgeevx(&balanc, &jobv, &jobv, &sense, &nn, A.data(), &nn, evals, evi.data(), Ql.data(), &nn, Q, &nn, &ilo,
+           &ihi, scl.data(), &abnrm, rce.data(), rcv.data(), &wq, &lwork, nullptr, &info, 1, 1, 1, 1);
+  int lw = (int)wq;
+  p_dgetri(&nn, nullptr, &nn, nullptr, &wq, &lwork, &info);
+  if ((int)wq > lw) lw = (int)wq;
+  std::vector<double> work(lw > 0 ? lw : 1);
+  memcpy(A.data(), S, sizeof(double) * n * n);
+  p_dgeevx(&balanc, &jobv, &jobv, &sense, &nn, A.data(), &nn, evals, evi.data(), Ql.data(), &nn, Q, &nn, &ilo,
+           &ihi, scl.data(), &abnrm, rce.data(), rcv.data(), work.data(), &lw, iwork.data(), &info, 1, 1, 1, 1);
+  if (info != 0) {
+    say("Error (LJMA_eigen 01): failed LAPACK call, code=%d\n", info);
+    return info;
+  }
+  for (int i = 0; i < n; i++)
+    if (evi[i] > 0) say("Error: imaginary part of eigenvalue %d found.\n", i + 1);
+  memcpy(Qinv, Q, sizeof(double) * n * n);
+  p_dgetrf(&nn, &nn, Qinv, &nn, ipiv.data(), &info);
+  if (info != 0) {
+    say("Error (LJMA_inverse 01): failed LAPACK call, code=%d\n", info);
+    return info;
+  }
+  p_dgetri(&nn, Qinv, &nn, ipiv.data(), work.data(), &lw, &info);
+  if (info != 0) say("Error (LJMA_inverse 03): failed LAPACK call, code=%d\n", info);
+  return info;
+}
+
+/* ======================================================== sweep parameters */
+/*
+ * Packed per-sweep block (pht_layout.h) from (S, s): the embedded chain
+ * exactly as src/PHT_MCMC_Aslett.c:279-297, the spectral data as :320-332
+ * (Q⁻¹v by reference-BLAS dgemv order), and the device-mode products with
+ * explicit fma in the order oracle/pht_oracle.c:orc_sp_build uses.
+ */
+static int build_params(int n, const double *S, const double *s, int method, std::vector<unsigned char> &out) {
+  const Layout L = make_layout(n);
+  out.assign(L.bytes(), 0);
+  double *d = reinterpret_cast<double *>(out.data());
+  int *iv = reinterpret_cast<int *>(out.data() + L.ndouble * 8);
+  double *P = d + L.P, *Pf = d + L.Pf, *Q = d + L.Q, *Qinv = d + L.Qinv, *ev = d + L.evals;
+  memcpy(d + L.S, S, sizeof(double) * n * n);
+  memcpy(d + L.s, s, sizeof(double) * n);
+  d[L.pi + 0] = 1.0;
+  for (int i = 0; i < n; i++) {
+    double rsum, rsumfull = 0.0;
+    for (int j = 0; j < n; j++) rsumfull += Pf[i + j * n] = P[i + j * n] = -S[i + j * n] / S[i + i * n];
+    rsum = rsumfull - P[i + i * n];
+    rsumfull += Pf[i + n * n] = -s[i] / S[i + i * n];
+    rsumfull -= Pf[i + i * n];
+    Pf[i + i * n] = P[i + i * n] = 0.0;
+    for (int j = 0; j < n; j++) {
+      P[i + j * n] = P[i + j * n] / rsum;
+      Pf[i + j * n] = Pf[i + j * n] / rsumfull;
+    }
+    Pf[i + n * n] = Pf[i + n * n] / rsumfull;
+  }
+  std::vector<double> Qs(n, 0.0), Q1(n, 0.0);
+  int info = 0;
+  if (method & (kMethodECS | kMethodDCS)) {
+    if (!lapack_ready()) {
+      set_err("no LAPACK bound (call pht_bind_lapack or set PHT_LAPACK_LIB)");
+      return -1;
+    }
+    info = eigen(n, S, ev, Q, Qinv);
+    /* dgemv 'N' (reference BLAS order): y = 0; y += x[c] * A[:,c] */
+    for (int c = 0; c < n; c++) {
+      const double ts = 1.0 * s[c], t1 = 1.0 * 1.0;
+      for (int r = 0; r < n; r++) {
+        Qs[r] = Qs[r] + ts * Qinv[r + c * n];
+        Q1[r] = Q1[r] + t1 * Qinv[r + c * n];
+      }
+    }
+  }
+  for (int j = 0; j < n; j++) {
+    const double Sjj = S[j + j * n];
+    d[L.logs + j] = s[j] > 0.0 ? pht_log(s[j]) : 0.0;
+    d[L.scale + j] = 1.0 / -Sjj;
+    d[L.logscale + j] = pht_log(d[L.scale + j]);
+    for (int i = 0; i < n; i++) {
+      double w = 0.0, v = 0.0;
+      for (int k = 0; k < n; k++) {
+        if (k != j) w = fma(S[j + k * n] / (-Sjj), Q[k + i * n], w);
+        v = fma(P[j + k * n], Q[k + i * n], v);
+      }
+      d[L.QQs + j + i * n] = Q[j + i * n] * Qs[i];
+      d[L.W + j + i * n] = w * Qs[i];
+      d[L.QQ1 + j + i * n] = Q[j + i * n] * Q1[i];
+      d[L.V + j + i * n] = v * Q1[i];
+    }
+  }
+  for (int i = 0; i < n; i++) {
+    double a = 0.0;
+    for (int k = 0; k < n; k++) a = fma(d[L.pi + k], Q[k + i * n], a);
+    d[L.piQ + i] = a;
+  }
+  for (int j = 0; j < n; j++) {
+    int a = 0, b = 0, c = 0;
+    for (int k = 0; k < n; k++) {
+      if (!(P[j + k * n] == 0.0)) iv[L.succP + j * n + a++] = k;
+      if (k != j && !(S[j + k * n] == 0.0)) iv[L.succS + j * n + c++] = k;
+    }
+    for (int k = 0; k <= n; k++)
+      if (!(Pf[j + k * n] == 0.0)) iv[L.succPf + j * (n + 1) + b++] = k;
+    iv[L.nsuccP + j] = a;
+    iv[L.nsuccPf + j] = b;
+    iv[L.nsuccS + j] = c;
+  }
+  return info;
+}
+
+extern "C" int pht_build_params(int n, const double *S, const double *s, int method, unsigned char *out,
+                                int out_bytes) {
+  std::vector<unsigned char> v;
+  int info = build_params(n, S, s, method, v);
+  if (info < 0) return info;
+  if ((int)v.size() > out_bytes) return -2;
+  memcpy(out, v.data(), v.size());
+  return info;
+}
+extern "C" int pht_params_bytes(int n) { return make_layout(n).bytes(); }
+extern "C" int pht_stats_len(int n) { return stats_len(n); }
+
+/* =========================================================== device shard */
+static int dispatch_method(int method) {
+  if (method & kMethodMHRS) return kMethodMHRS;
+  if (method & kMethodDCS) return kMethodDCS;
+  if (method & kMethodECS) return kMethodECS;
+  return 0;
+}
+
+struct pht_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int n = 0, method = 0, mhit = 1;
+  long count = 0;
+  double *d_y = nullptr;
+  int *d_cens = nullptr;
+  uint32_t *d_gid = nullptr;
+  unsigned char *d_params = nullptr;
+  unsigned long long *d_stats = nullptr;
+  unsigned long long *h_stats = nullptr; /* pinned */
+  unsigned char *h_params = nullptr;     /* pinned */
+  std::vector<long> order;               /* sorted position -> local index */
+  /* debug buffers */
+  long long *d_zq = nullptr;
+  int *d_N = nullptr, *d_B = nullptr, *d_pre = nullptr, *d_flags = nullptr;
+  uint32_t *d_ndraw = nullptr;
+  long dbg_cap = 0;
+  float last_ms = 0.f;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+static void ctx_free_obs(pht_ctx *c) {
+  (void)hipSetDevice(c->device);
+  if (c->d_y) (void)hipFree(c->d_y);
+  if (c->d_cens) (void)hipFree(c->d_cens);
+  if (c->d_gid) (void)hipFree(c->d_gid);
+  c->d_y = nullptr; c->d_cens = nullptr; c->d_gid = nullptr;
+}
+static void ctx_free_dbg(pht_ctx *c) {
+  (void)hipSetDevice(c->device);
+  if (c->d_zq) (void)hipFree(c->d_zq);
+  if (c->d_N) (void)hipFree(c->d_N);
+  if (c->d_B) (void)hipFree(c->d_B);
+  if (c->d_pre) (void)hipFree(c->d_pre);
+  if (c->d_flags) (void)hipFree(c->d_flags);
+  if (c->d_ndraw) (void)hipFree(c->d_ndraw);
+  c->d_zq = nullptr; c->d_N = nullptr; c->d_B = c->d_pre = c->d_flags = nullptr; c->d_ndraw = nullptr;
+  c->dbg_cap = 0;
+}
+
+extern "C" int pht_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+extern "C" pht_ctx *pht_ctx_create(int device, int n, int method, int mhit) {
+  if (n < 1 || n > kMaxN) {
+    set_err("n=%d outside 1..%d", n, kMaxN);
+    return nullptr;
+  }
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) {
+    set_err("no HIP device available (%s)", hipGetErrorString(e));
+    return nullptr;
+  }
+  if (device < 0 || device >= ndev) {
+    set_err("device %d out of range (%d devices)", device, ndev);
+    return nullptr;
+  }
+  pht_ctx *c = new pht_ctx();
+  c->device = device;
+  c->n = n;
+  c->method = dispatch_method(method);
+  c->mhit = mhit;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->d_params, make_layout(n).bytes()) != hipSuccess ||
+      hipMalloc(&c->d_stats, sizeof(unsigned long long) * stats_len(n)) != hipSuccess ||
+      hipHostMalloc(&c->h_stats, sizeof(unsigned long long) * stats_len(n), 0) != hipSuccess ||
+      hipHostMalloc(&c->h_params, make_layout(n).bytes(), 0) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    set_err("device %d: HIP allocation failed", device);
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+extern "C" void pht_ctx_destroy(pht_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  ctx_free_obs(c);
+  ctx_free_dbg(c);
+  if (c->d_params) (void)hipFree(c->d_params);
+  if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->h_stats) (void)hipHostFree(c->h_stats);
+  if (c->h_params) (void)hipHostFree(c->h_params);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+/*
+ * Upload this shard's observations.  obs0 = global index of y[0]; the
+ * Philox counter of observation i is obs0 + i whatever the shard layout.
+ * Observations are reordered on the device (exact before censored, then by
+ * y) so a wavefront's lanes carry similar path lengths; results do not
+ * depend on the order.
+ */
+extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, long count, long obs0) {
+  HIPCHK(hipSetDevice(c->device));
+  ctx_free_obs(c);
+  ctx_free_dbg(c);
+  c->count = count;
+  if (count == 0) return 0;
+  std::vector<long> ord(count);
+  std::iota(ord.begin(), ord.end(), 0L);
+  std::stable_sort(ord.begin(), ord.end(), [&](long a, long b) {
+    const int ca = cens[a] != 0, cb = cens[b] != 0;
+    if (ca != cb) return ca < cb;
+    return y[a] < y[b];
+  });
+  std::vector<double> ys(count);
+  std::vector<int> cs(count);
+  std::vector<uint32_t> gs(count);
+  for (long k = 0; k < count; k++) {
+    ys[k] = y[ord[k]];
+    cs[k] = cens[ord[k]];
+    gs[k] = (uint32_t)(obs0 + ord[k]);
+  }
+  c->order = std::move(ord);
+  HIPCHK(hipMalloc(&c->d_y, sizeof(double) * count));
+  HIPCHK(hipMalloc(&c->d_cens, sizeof(int) * count));
+  HIPCHK(hipMalloc(&c->d_gid, sizeof(uint32_t) * count));
+  HIPCHK(hipMemcpy(c->d_y, ys.data(), sizeof(double) * count, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->d_cens, cs.data(), sizeof(int) * count, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->d_gid, gs.data(), sizeof(uint32_t) * count, hipMemcpyHostToDevice));
+  return 0;
+}
+
+/* enqueue one sweep (params already in c->h_params); stats -> c->h_stats */
+static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int zexp, bool debug) {
+  HIPCHK(hipSetDevice(c->device));
+  const int pb = make_layout(c->n).bytes();
+  const int sl = stats_len(c->n);
+  HIPCHK(hipMemcpyAsync(c->d_params, c->h_params, pb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * sl, c->stream));
+  SweepArgs a;
+  memset(&a, 0, sizeof a);
+  a.params = c->d_params;
+  a.n = c->n;
+  a.mhit = c->mhit;
+  a.count = c->count;
+  a.y = c->d_y;
+  a.cens = c->d_cens;
+  a.gid = c->d_gid;
+  a.k0 = k0;
+  a.k1 = k1;
+  a.sweep = sweep;
+  a.zscale = ldexp(1.0, zexp);
+  a.stats = c->d_stats;
+  if (debug) {
+    if (c->dbg_cap < c->count) {
+      ctx_free_dbg(c);
+      HIPCHK(hipMalloc(&c->d_zq, sizeof(long long) * c->count * c->n));
+      HIPCHK(hipMalloc(&c->d_N, sizeof(int) * c->count * c->n * c->n));
+      HIPCHK(hipMalloc(&c->d_B, sizeof(int) * c->count));
+      HIPCHK(hipMalloc(&c->d_pre, sizeof(int) * c->count));
+      HIPCHK(hipMalloc(&c->d_flags, sizeof(int) * c->count));
+      HIPCHK(hipMalloc(&c->d_ndraw, sizeof(uint32_t) * c->count));
+      c->dbg_cap = c->count;
+    }
+    HIPCHK(hipMemsetAsync(c->d_zq, 0, sizeof(long long) * c->count * c->n, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_N, 0, sizeof(int) * c->count * c->n * c->n, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_B, 0, sizeof(int) * c->count, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_pre, 0, sizeof(int) * c->count, c->stream));
+    a.dbg_zq = c->d_zq;
+    a.dbg_N = c->d_N;
+    a.dbg_B = c->d_B;
+    a.dbg_pre = c->d_pre;
+    a.dbg_flags = c->d_flags;
+    a.dbg_ndraw = c->d_ndraw;
+  }
+  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  HIPCHK(pht_launch_sweep(&a, c->method, debug ? 1 : 0, c->stream));
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  HIPCHK(hipMemcpyAsync(c->h_stats, c->d_stats, sizeof(unsigned long long) * sl, hipMemcpyDeviceToHost, c->stream));
+  return 0;
+}
+
+static int ctx_wait(pht_ctx *c) {
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  return 0;
+}
+
+extern "C" int pht_ctx_sweep(pht_ctx *c, const double *S, const double *s, uint32_t k0, uint32_t k1,
+                             uint32_t sweep, int zexp, long long *stats_out) {
+  std::vector<unsigned char> pb;
+  int info = build_params(c->n, S, s, c->method, pb);
+  if (info < 0) return info;
+  memcpy(c->h_params, pb.data(), pb.size());
+  if (ctx_enqueue(c, k0, k1, sweep, zexp, false) || ctx_wait(c)) return -1;
+  memcpy(stats_out, c->h_stats, sizeof(long long) * stats_len(c->n));
+  return 0;
+}
+
+/* Per-observation debug sweep: outputs in the caller's original observation
+ * order (B, pre, flags, ndraw [count]; zq [count*n]; N [count*n*n], N[i + j n]). */
+extern "C" int pht_ctx_sweep_debug(pht_ctx *c, const double *S, const double *s, uint32_t k0, uint32_t k1,
+                                   uint32_t sweep, int zexp, long long *stats_out, int *B, int *pre, int *flags,
+                                   uint32_t *ndraw, long long *zq, int *N) {
+  std::vector<unsigned char> pb;
+  int info = build_params(c->n, S, s, c->method, pb);
+  if (info < 0) return info;
+  memcpy(c->h_params, pb.data(), pb.size());
+  if (ctx_enqueue(c, k0, k1, sweep, zexp, true) || ctx_wait(c)) return -1;
+  memcpy(stats_out, c->h_stats, sizeof(long long) * stats_len(c->n));
+  const long cnt = c->count;
+  const int n = c->n;
+  std::vector<long long> hz(cnt * n);
+  std::vector<int> hN(cnt * n * n), hB(cnt), hp(cnt), hf(cnt);
+  std::vector<uint32_t> hd(cnt);
+  HIPCHK(hipMemcpy(hz.data(), c->d_zq, sizeof(long long) * cnt * n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(hN.data(), c->d_N, sizeof(int) * cnt * n * n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(hB.data(), c->d_B, sizeof(int) * cnt, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(hp.data(), c->d_pre, sizeof(int) * cnt, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(hf.data(), c->d_flags, sizeof(int) * cnt, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(hd.data(), c->d_ndraw, sizeof(uint32_t) * cnt, hipMemcpyDeviceToHost));
+  for (long k = 0; k < cnt; k++) {
+    const long o = c->order[k];
+    B[o] = hB[k];
+    pre[o] = hp[k];
+    flags[o] = hf[k];
+    ndraw[o] = hd[k];
+    memcpy(zq + o * n, hz.data() + k * n, sizeof(long long) * n);
+    memcpy(N + o * n * n, hN.data() + k * n * n, sizeof(int) * n * n);
+  }
+  return 0;
+}
+
+extern "C" float pht_ctx_last_kernel_ms(pht_ctx *c) { return c->last_ms; }
+
+/* fixed-point exponent for z (52 - ceil(log2(sum y + 1))) */
+extern "C" int pht_zexp(const double *y, long l) {
+  double sy = 0.0;
+  for (long i = 0; i < l; i++) sy += y[i];
+  return 52 - (int)ceil(log2(sy + 1.0));
+}
+
+/* ============================================================ Gibbs core */
+namespace {
+struct Ent {
+  int i, j;
+  double c;
+};
+
+/* The reference's Gibbs bookkeeping (src/PHT_MCMC_Aslett.c:187-405) with
+ * the linked lists kept as arrays visited in list (reverse-insertion)
+ * order, so zsum and the diagonal refresh sum in the reference's order. */
+struct GibbsState {
+  int it, n, m, n1;
+  const double *nu, *zeta;
+  double *res;
+  std::vector<double> TT, S, s;
+  std::vector<std::vector<Ent>> Nl, Sl, sl, zl, TTl, Dl;
+
+  GibbsState(int it_, int n_, int m_, const double *nu_, const double *zeta_, const int *T, const double *C,
+             const double *start, double *res_)
+      : it(it_), n(n_), m(m_), n1(n_ + 1), nu(nu_), zeta(zeta_), res(res_) {
+    RHost &R = rhost();
+    TT.assign(n1 * n1, 0.0);
+    S.assign(n * n, 0.0);
+    s.assign(n, 0.0);
+    Nl.resize(m); Sl.resize(m); sl.resize(m); zl.resize(m); TTl.resize(m); Dl.resize(n1);
+    if (start[0] < 0) {
+      for (int i = 0; i < m; i++)
+        res[0 + (size_t)i * it] = (nu[i] > 1) ? (nu[i] - 1.0) / zeta[i] : R.gamma(nu[i], 1.0 / zeta[i]);
+    } else {
+      for (int i = 0; i < m; i++) res[0 + (size_t)i * it] = start[i];
+    }
+    double rsum = 0.0;
+    for (int i = 0; i < n1; i++) {
+      for (int j = 0; j < n1; j++) {
+        const int t = T[i + j * n1];
+        if (t == 0) {
+          TT[i + j * n1] = 0.0;
+          continue;
+        }
+        const int k = t - 1;
+        const double c = C[i + j * n1];
+        rsum -= TT[i + j * n1] = res[0 + (size_t)k * it] * c;
+        if (j == n) {
+          Nl[k].push_back({i, i, 1.0});
+          sl[k].push_back({i, 0, c});
+        } else {
+          Nl[k].push_back({i, j, 1.0});
+          Sl[k].push_back({i, j, c});
+        }
+        zl[k].push_back({i, 0, c});
+        TTl[k].push_back({i, j, c});
+        Dl[i].push_back({i, j, 1.0});
+      }
+      TT[i + i * n1] = rsum;
+      rsum = 0.0;
+    }
+    for (int i = 0; i < n; i++)
+      for (int j = 0; j < n; j++) S[i + j * n] = TT[i + j * n1];
+    for (int i = 0; i < n; i++) s[i] = TT[i + n * n1];
+  }
+
+  /* steps 4-5 (:340-397): compile statistics and draw from the posteriors */
+  void update(int iter, const double *z, const long long *Nt) {
+    RHost &R = rhost();
+    std::vector<long long> Nsum(m, 0);
+    std::vector<double> zsum(m, 0.0);
+    for (int k = 0; k < m; k++) {
+      for (int e = (int)Nl[k].size() - 1; e >= 0; e--) Nsum[k] += Nt[Nl[k][e].i + Nl[k][e].j * n];
+      for (int e = (int)zl[k].size() - 1; e >= 0; e--) zsum[k] += z[zl[k][e].i] / zl[k][e].c;
+    }
+    for (int k = 0; k < m; k++) {
+      const double tmp = res[iter + (size_t)k * it] =
+          R.gamma(nu[k] + (double)(int)Nsum[k], 1.0 / (zeta[k] + zsum[k]));
+      for (int e = (int)TTl[k].size() - 1; e >= 0; e--) TT[TTl[k][e].i + TTl[k][e].j * n1] = tmp * TTl[k][e].c;
+      for (int e = (int)Sl[k].size() - 1; e >= 0; e--) S[Sl[k][e].i + Sl[k][e].j * n] = tmp * Sl[k][e].c;
+      for (int e = (int)sl[k].size() - 1; e >= 0; e--) s[sl[k][e].i] = tmp * sl[k][e].c;
+    }
+    for (int i = 0; i < n; i++) {
+      double tmp = 0.0;
+      for (int e = (int)Dl[i].size() - 1; e >= 0; e--) tmp -= TT[Dl[i][e].i + Dl[i][e].j * n1];
+      TT[i + i * n1] = tmp;
+      S[i + i * n] = tmp;
+    }
+  }
+};
+
+/* Run the Gibbs loop over a set of device shards; reduce = optional
+ * cross-process all-reduce of the int64 statistics block. */
+int gibbs_run(int it, int mhit, int method, int n, int m, const double *nu, const double *zeta, const int *T,
+              const double *C, const double *y, long l, int silent, const double *start, double *res,
+              std::vector<pht_ctx *> &ctxs, uint32_t k0, uint32_t k1, int zexp, pht_reduce_fn reduce,
+              void *reduce_user, double *kernel_ms_total) {
+  (void)y; (void)l; (void)mhit;
+  GibbsState G(it, n, m, nu, zeta, T, C, start, res);
+  const int disp = dispatch_method(method);
+  const int sl = stats_len(n);
+  std::vector<long long> tot(sl);
+  std::vector<double> z(n);
+  std::vector<unsigned char> pb;
+  say("Starting phase-type MCMC sampler ...\n\nBegining processing ...");
+  if (silent) say(" silent processing selected, there will be no further feedback until MCMC run complete");
+  double kms = 0.0;
+  for (int iter = 1; iter < it; iter++) {
+    if (!silent) say("\rProcessing iteration %d of %d (%.1lf%%)\r", iter + 1, it, (100.0 * (iter + 1)) / it);
+    if (!disp) {
+      say("CRITICAL ERROR: Unknown sampling method (code = %d)\n\n", method);
+      continue;
+    }
+    const int info = build_params(n, G.S.data(), G.s.data(), disp == kMethodMHRS ? kMethodMHRS : method, pb);
+    if (info < 0) return -1;
+    for (pht_ctx *c : ctxs) {
+      memcpy(c->h_params, pb.data(), pb.size());
+      if (ctx_enqueue(c, k0, k1, (uint32_t)iter, zexp, false)) return -1;
+    }
+    std::fill(tot.begin(), tot.end(), 0LL);
+    for (pht_ctx *c : ctxs) {
+      if (ctx_wait(c)) return -1;
+      kms += c->last_ms;
+      for (int k = 0; k < sl; k++) tot[k] += (long long)c->h_stats[k];
+    }
+    if (reduce && reduce(tot.data(), sl, reduce_user) != 0) {
+      set_err("statistics all-reduce callback failed at sweep %d", iter);
+      return -1;
+    }
+    for (int k = 0; k < n; k++) z[k] = ldexp((double)tot[k], -zexp);
+    G.update(iter, z.data(), tot.data() + 2 * n);
+  }
+  if (kernel_ms_total) *kernel_ms_total = kms;
+  return 0;
+}
+}  // namespace
+
+/*
+ * Multi-process entry (one process per GPU): this process owns observations
+ * [obs0, obs0 + l) of a data set of l_total observations (zexp must be the
+ * same on every rank: pht_zexp over all observations); `reduce` sums the
+ * statistics block across ranks (e.g. an RCCL all-reduce).  The R-stream
+ * (pht_set_seed) must be seeded identically on all ranks; every rank then
+ * draws identical Gamma updates and the chain is the single-process chain.
+ */
+extern "C" int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double *nu, const double *zeta,
+                             const int *T, const double *C, int zexp, int silent, const double *start, double *res,
+                             pht_reduce_fn reduce, void *reduce_user, double *kernel_ms_total) {
+  RHost &R = rhost();
+  R.begin();
+  const uint32_t k0 = (uint32_t)(R.u() * 4294967296.0);
+  const uint32_t k1 = (uint32_t)(R.u() * 4294967296.0);
+  std::vector<pht_ctx *> ctxs{c};
+  int rc = gibbs_run(it, c->mhit, method, c->n, m, nu, zeta, T, C, nullptr, c->count, silent, start, res, ctxs, k0,
+                     k1, zexp, reduce, reduce_user, kernel_ms_total);
+  R.end();
+  return rc;
+}
+
+/* ======================================================= .C entry point */
+/*
+ * Drop-in replacement of LJMA_Gibbs (src/PHT_MCMC_Aslett.c:104): same 15
+ * arguments, same semantics and output (res[iter + i*it]).  Observations are
+ * sharded over all visible GPUs (PHT_DEVICES=k limits the count).
+ * Divergences, documented in DESIGN.md: per-observation draws come from
+ * Philox (keyed by two R-stream uniforms drawn at entry) instead of R's
+ * serial stream; z is reduced in exact fixed point.
+ */
+extern "C" void LJMA_Gibbs(int *it, int *mhit, int *method, int *n, int *m, double *nu, double *zeta, int *T,
+                           double *C, double *y, int *l, int *censored, double *start, int *silent, double *res) {
+  RHost &R = rhost();
+  g_err.clear();
+  R.begin();
+  const uint32_t k0 = (uint32_t)(R.u() * 4294967296.0);
+  const uint32_t k1 = (uint32_t)(R.u() * 4294967296.0);
+  const int zexp = pht_zexp(y, *l);
+  say("Setting up Gibbs run ...\n");
+  int ndev = pht_device_count();
+  if (const char *e = getenv("PHT_DEVICES")) ndev = std::min(ndev, atoi(e));
+  std::vector<pht_ctx *> ctxs;
+  int rc = 0;
+  if (ndev <= 0) {
+    set_err("PhaseType (MI355X): no HIP device available");
+    rc = -1;
+  }
+  const long L = *l;
+  for (int d = 0; d < ndev && rc == 0; d++) {
+    const long lo = L * d / ndev, hi = L * (d + 1) / ndev;
+    pht_ctx *c = pht_ctx_create(d, *n, *method, *mhit);
+    if (!c) {
+      rc = -1;
+      break;
+    }
+    ctxs.push_back(c);
+    if (pht_ctx_set_obs(c, y + lo, censored + lo, hi - lo, lo)) rc = -1;
+  }
+  if (rc == 0)
+    rc = gibbs_run(*it, *mhit, *method, *n, *m, nu, zeta, T, C, y, L, *silent, start, res, ctxs, k0, k1, zexp,
+                   nullptr, nullptr, nullptr);
+  for (pht_ctx *c : ctxs) pht_ctx_destroy(c);
+  if (rc == 0) say("\n\nCompleted MCMC run, returning results ...\n");
+  R.end();
+  if (rc != 0) {
+    if (R.inR && R.rerror) R.rerror("%s", g_err.c_str());
+    fprintf(stderr, "PhaseType (MI355X): %s\n", g_err.c_str());
+  }
+}
+
+/* ================================================== R native registration */
+/* R's registration ABI (R_ext/Rdynload.h), declared here so the library
+ * also loads outside R; the R functions are resolved only when present. */
+extern "C" {
+typedef void *(*pht_DL_FUNC)(void);
+typedef unsigned int pht_R_NativePrimitiveArgType;
+typedef struct {
+  const char *name;
+  pht_DL_FUNC fun;
+  int numArgs;
+  pht_R_NativePrimitiveArgType *types;
+} pht_R_CMethodDef;
+}
+
+extern "C" void R_init_PhaseType(void *dll) {
+  /* INTSXP = 13, REALSXP = 14 (src/Registrations.c:6-9) */
+  static pht_R_NativePrimitiveArgType types[15] = {13, 13, 13, 13, 13, 14, 14, 13, 14, 14, 13, 13, 14, 13, 14};
+  static pht_R_CMethodDef cMethods[] = {{"LJMA_Gibbs", (pht_DL_FUNC)&LJMA_Gibbs, 15, types},
+                                        {nullptr, nullptr, 0, nullptr}};
+  typedef int (*reg_fn)(void *, const pht_R_CMethodDef *, const void *, const void *, const void *);
+  typedef int (*bool_fn)(void *, int);
+  reg_fn reg = (reg_fn)dlsym(RTLD_DEFAULT, "R_registerRoutines");
+  bool_fn dyn = (bool_fn)dlsym(RTLD_DEFAULT, "R_useDynamicSymbols");
+  bool_fn force = (bool_fn)dlsym(RTLD_DEFAULT, "R_forceSymbols");
+  if (!reg || !dyn || !force) return;
+  reg(dll, cMethods, nullptr, nullptr, nullptr);
+  dyn(dll, 0);
+  force(dll, 1);
+}

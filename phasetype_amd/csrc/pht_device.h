@@ -1,0 +1,826 @@
+/*
+ * pht_device.h — per-observation latent-path samplers for one GPU lane.
+ *
+ * Each function follows the device specification restated on the CPU in
+ * oracle/pht_oracle_impl.h (ORC_DEV == 1) operation for operation, so a
+ * lane and the oracle produce bit-identical (B, z, N) for the same
+ * observation, Philox key, sweep and parameters.  Reference provenance:
+ *   ecs_exact      LJMA_samplechain_Aslett2  src/Simulate_AbsCTMC_eq_Aslett_ECS.c:205-373
+ *                  (+ LJMA_probAbsorb :120-136, LJMA_ECS_dens :150-171, LJMA_moveMass :21-41)
+ *   censored       LJMA_samplechain / LJMA_condjump_r_ars / LJMA_condjumpdens
+ *                  src/Simulate_AbsCTMC_gt_Aslett_DCS.c:111-418
+ *   mhrs           LJMA_MHsample_Bladt + LJMA_samplechain_Bladt
+ *                  src/Simulate_AbsCTMC_eq_Bladt_MHRS.c:37-117, src/Simulate_AbsCTMC_gt_Bladt_MHRS.c:151-277
+ *   dcs            LJMA_Hobolth_endState + LJMA_samplechain_Hobolth + HobCDF + Find02
+ *                  src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:11-51, src/Simulate_AbsCTMC_gt_Hobolth_DCS.c:23-226,
+ *                  src/utility.c:233-338
+ *   arms           src/arms.c:115-812 (metropolis on, ninit 4, npoint 100)
+ *
+ * Template parameter NT: compile-time number of transient states (NT > 0:
+ * fully unrolled loops, small vectors in registers) or 0 (runtime n).
+ * Env: ARMS envelope storage policy (pht_env.h).
+ */
+#ifndef PHT_DEVICE_H
+#define PHT_DEVICE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pht_detmath.h"
+#include "pht_layout.h"
+#include "pht_philox.h"
+
+namespace pht {
+
+/* flag bits (per observation) */
+constexpr int kFlagScanEnd = 1;    /* categorical scan ran past the last candidate */
+constexpr int kFlagDcsZero = 2;    /* DCS jump weights summed to 0 / NaN */
+constexpr int kFlagArmsCap = 4;    /* ARMS iteration cap */
+constexpr int kFlagJumpCap = 8;    /* path length cap */
+constexpr int kFlagMhrsCap = 16;   /* MHRS rejection-attempt cap */
+constexpr int kFlagArmsErr = 32;   /* ARMS initial-point error (1003/1004/1007) */
+
+constexpr int kArmsNPoint = 100;
+constexpr int kArmsMaxIt = 10000;
+constexpr int kMaxJumps = 1 << 20;
+constexpr int kMhrsMaxAtt = 1 << 22;
+constexpr double kXEps = 0.00001, kYEps = 0.1, kEYEps = 0.001, kYCeil = 50.;
+
+/* parameter block accessor (pointers into LDS or global memory) */
+template <int NT>
+struct Par {
+  const double *d;
+  const int *iv;
+  Layout L;
+  __device__ __forceinline__ int n() const { return NT > 0 ? NT : L.n; }
+  __device__ __forceinline__ double evals(int i) const { return d[L.evals + i]; }
+  __device__ __forceinline__ double s(int i) const { return d[L.s + i]; }
+  __device__ __forceinline__ double logs(int i) const { return d[L.logs + i]; }
+  __device__ __forceinline__ double scale(int i) const { return d[L.scale + i]; }
+  __device__ __forceinline__ double logscale(int i) const { return d[L.logscale + i]; }
+  __device__ __forceinline__ double piQ(int i) const { return d[L.piQ + i]; }
+  __device__ __forceinline__ double pi(int i) const { return d[L.pi + i]; }
+  __device__ __forceinline__ double S(int i, int j) const { return d[L.S + i + j * n()]; }
+  __device__ __forceinline__ double P(int i, int j) const { return d[L.P + i + j * n()]; }
+  __device__ __forceinline__ double Pf(int i, int j) const { return d[L.Pf + i + j * n()]; }
+  __device__ __forceinline__ double QQs(int i, int j) const { return d[L.QQs + i + j * n()]; }
+  __device__ __forceinline__ double W(int i, int j) const { return d[L.W + i + j * n()]; }
+  __device__ __forceinline__ double QQ1(int i, int j) const { return d[L.QQ1 + i + j * n()]; }
+  __device__ __forceinline__ double V(int i, int j) const { return d[L.V + i + j * n()]; }
+  __device__ __forceinline__ double Q(int i, int j) const { return d[L.Q + i + j * n()]; }
+  __device__ __forceinline__ double Qinv(int i, int j) const { return d[L.Qinv + i + j * n()]; }
+  __device__ __forceinline__ int nsuccP(int j) const { return iv[L.nsuccP + j]; }
+  __device__ __forceinline__ int succP(int j, int q) const { return iv[L.succP + j * n() + q]; }
+  __device__ __forceinline__ int nsuccPf(int j) const { return iv[L.nsuccPf + j]; }
+  __device__ __forceinline__ int succPf(int j, int q) const { return iv[L.succPf + j * (n() + 1) + q]; }
+  __device__ __forceinline__ int nsuccS(int j) const { return iv[L.nsuccS + j]; }
+  __device__ __forceinline__ int succS(int j, int q) const { return iv[L.succS + j * n() + q]; }
+};
+
+#define PHT_VEC(NT) ((NT) > 0 ? (NT) : kMaxN)
+
+/* per-lane random stream helpers (oracle: orcD_u / orcD_runif / orcD_rexp) */
+__device__ __forceinline__ double dev_u(pht_stream &r) { return pht_next_u(&r); }
+__device__ __forceinline__ double dev_runif(pht_stream &r, double a, double b) {
+  if (!isfinite(a) || !isfinite(b) || b < a) return __builtin_nan("");
+  if (a == b) return a;
+  return a + (b - a) * pht_next_u(&r);
+}
+__device__ __forceinline__ double dev_rexp(pht_stream &r, double scale) {
+  if (!isfinite(scale) || scale <= 0.0) return scale == 0.0 ? 0.0 : __builtin_nan("");
+  return scale * -pht_log(pht_next_u(&r));
+}
+
+/* Lane context: random stream, flags and counters of the current observation. */
+struct Lane {
+  pht_stream r;
+  int flags;
+  int neval;
+  int nbrent;
+  int njump;
+};
+
+/* ===================================================================== ARMS */
+template <class Env>
+__device__ __forceinline__ double expshift(double y, double y0) {
+  return (y - y0 > -2.0 * kYCeil) ? pht_exp(y - y0 + kYCeil) : 0.0;
+}
+__device__ __forceinline__ double logshift(double y, double y0) { return pht_log(y) + y0 - kYCeil; }
+
+template <class Env>
+__device__ void arms_meet(Env &e, int k) {
+  double gl = 0.0, gr = 0.0, grl = 0.0, dl = 0.0, dr = 0.0;
+  const int last = e.cnt - 1;
+  const bool il = (k >= 3), ir = (k + 3 <= last), irl = (k >= 1 && k + 1 <= last);
+  if (il) gl = (e.Y(k - 1) - e.Y(k - 3)) / (e.X(k - 1) - e.X(k - 3));
+  if (ir) gr = (e.Y(k + 1) - e.Y(k + 3)) / (e.X(k + 1) - e.X(k + 3));
+  if (irl) grl = (e.Y(k + 1) - e.Y(k - 1)) / (e.X(k + 1) - e.X(k - 1));
+  if (irl && il && (gl < grl)) gl = gl + (1.0 + 1.0) * (grl - gl);
+  if (irl && ir && (gr > grl)) gr = gr + (1.0 + 1.0) * (grl - gr);
+  if (il && irl) {
+    dr = (gl - grl) * (e.X(k + 1) - e.X(k - 1));
+    if (dr < kYEps) dr = kYEps;
+  }
+  if (ir && irl) {
+    dl = (grl - gr) * (e.X(k + 1) - e.X(k - 1));
+    if (dl < kYEps) dl = kYEps;
+  }
+  if (il && ir && irl) {
+    const double xr = e.X(k + 1), xl = e.X(k - 1), yr = e.Y(k + 1), yl = e.Y(k - 1);
+    e.X(k) = (dl * xr + dr * xl) / (dl + dr);
+    e.Y(k) = (dl * yr + dr * yl + dl * dr) / (dl + dr);
+  } else if (il && irl) {
+    e.X(k) = e.X(k + 1);
+    e.Y(k) = e.Y(k + 1) + dr;
+  } else if (ir && irl) {
+    e.X(k) = e.X(k - 1);
+    e.Y(k) = e.Y(k - 1) + dl;
+  } else if (il) {
+    e.Y(k) = e.Y(k - 1) + gl * (e.X(k) - e.X(k - 1));
+  } else if (ir) {
+    e.Y(k) = e.Y(k + 1) - gr * (e.X(k + 1) - e.X(k));
+  }
+}
+
+template <class Env>
+__device__ void arms_cumulate(Env &e) {
+  double ymax = e.Y(0);
+  for (int k = 1; k < e.cnt; k++) {
+    const double yk = e.Y(k);
+    if (yk > ymax) ymax = yk;
+  }
+  e.ymax = ymax;
+  double eyp = expshift<Env>(e.Y(0), ymax), xp = e.X(0), yp = e.Y(0);
+  e.EY(0) = eyp;
+  double cum = 0.;
+  e.CUM(0) = cum;
+  for (int k = 1; k < e.cnt; k++) {
+    const double xk = e.X(k), yk = e.Y(k);
+    const double eyk = expshift<Env>(yk, ymax);
+    e.EY(k) = eyk;
+    double a;
+    if (xp == xk) a = 0.;
+    else if (fabs(yk - yp) < kYEps) a = 0.5 * (eyk + eyp) * (xk - xp);
+    else a = ((eyk - eyp) / (yk - yp)) * (xk - xp);
+    cum = cum + a;
+    e.CUM(k) = cum;
+    xp = xk; yp = yk; eyp = eyk;
+  }
+}
+
+struct WPt {
+  double x, y, ey;
+  int pr;
+};
+
+template <class Env>
+__device__ void arms_invert(Env &e, double prob, WPt &p) {
+  int q = e.cnt - 1;
+  const double u = prob * e.CUM(q);
+  double cl = e.CUM(q - 1);
+  while (cl > u) {
+    q--;
+    cl = e.CUM(q - 1);
+  }
+  p.pr = q;
+  const double cr = e.CUM(q);
+  const double prop = (u - cl) / (cr - cl);
+  const double xl = e.X(q - 1), xr = e.X(q);
+  if (xl == xr) {
+    p.x = xr; p.y = e.Y(q); p.ey = e.EY(q);
+    return;
+  }
+  const double yl = e.Y(q - 1), yr = e.Y(q), eyl = e.EY(q - 1), eyr = e.EY(q);
+  if (fabs(yr - yl) < kYEps) {
+    if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
+      p.x = xl + ((xr - xl) / (eyr - eyl)) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
+    else
+      p.x = xl + (xr - xl) * prop;
+    p.ey = ((p.x - xl) / (xr - xl)) * (eyr - eyl) + eyl;
+    p.y = logshift(p.ey, e.ymax);
+  } else {
+    p.x = xl + ((xr - xl) / (yr - yl)) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
+    p.y = ((p.x - xl) / (xr - xl)) * (yr - yl) + yl;
+    p.ey = expshift<Env>(p.y, e.ymax);
+  }
+}
+
+template <class Env, class F>
+__device__ void arms_update(Env &e, const WPt &p, F &f, Lane &ln) {
+  if (e.cnt > kArmsNPoint - 2) return;
+  const int pr = p.pr;
+  for (int k = e.cnt - 1; k >= pr; k--) {
+    e.X(k + 2) = e.X(k);
+    e.Y(k + 2) = e.Y(k);
+  }
+  e.cnt += 2;
+  const int qi = ((pr - 1) & 1) ? pr + 1 : pr;
+  e.X(qi) = p.x;
+  e.Y(qi) = p.y;
+  const int ql = (qi >= 2) ? qi - 2 : qi - 1;
+  const int qr = (qi + 2 <= e.cnt - 1) ? qi + 2 : qi + 1;
+  const double xl = e.X(ql), xr = e.X(qr);
+  if (p.x < (1. - kXEps) * xl + kXEps * xr) {
+    const double xn = (1. - kXEps) * xl + kXEps * xr;
+    e.X(qi) = xn;
+    e.Y(qi) = f(xn);
+    ln.neval++;
+  } else if (p.x > kXEps * xl + (1. - kXEps) * xr) {
+    const double xn = kXEps * xl + (1. - kXEps) * xr;
+    e.X(qi) = xn;
+    e.Y(qi) = f(xn);
+    ln.neval++;
+  }
+  arms_meet(e, qi - 1);
+  arms_meet(e, qi + 1);
+  if (qi >= 2) arms_meet(e, qi - 3);
+  if (qi + 2 <= e.cnt - 1) arms_meet(e, qi + 3);
+  arms_cumulate(e);
+}
+
+/* arms() as used by the reference (xprev 0, one sample).  Returns 0, an
+ * initial-point error code, or 4 on the iteration cap. */
+template <class Env, class F>
+__device__ int arms(Env &e, const double xinit[4], double xl, double xr, F &f, double xprev, double &xsamp,
+                    Lane &ln) {
+  if ((xinit[0] <= xl) || (xinit[3] >= xr)) return 1003;
+  if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) return 1004;
+  e.cnt = 9;
+  e.X(0) = xl;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    e.X(2 * k + 1) = xinit[k];
+    e.Y(2 * k + 1) = f(xinit[k]);
+  }
+  ln.neval += 4;
+  e.X(8) = xr;
+#pragma unroll
+  for (int k = 0; k < 9; k += 2) arms_meet(e, k);
+  arms_cumulate(e);
+  if ((xprev < xl) || (xprev > xr)) return 1007;
+  const double yprev = f(xprev);
+  ln.neval++;
+  for (int it = 0;; it++) {
+    if (it >= kArmsMaxIt) {
+      xsamp = xprev;
+      return 4;
+    }
+    WPt p;
+    arms_invert(e, dev_u(ln.r), p);
+    const double u = dev_u(ln.r) * p.ey;
+    const double y = logshift(u, e.ymax);
+    const double ynew = f(p.x);
+    ln.neval++;
+    if (y >= ynew) {
+      p.y = ynew;
+      p.ey = expshift<Env>(p.y, e.ymax);
+      arms_update(e, p, f, ln);
+      continue;
+    }
+    int ql = 0;
+    while (e.X(ql + 1) < xprev) ql++;
+    const int qr = ql + 1;
+    const double xql = e.X(ql), yql = e.Y(ql);
+    double w = (xprev - xql) / (e.X(qr) - xql);
+    double zold = yql + w * (e.Y(qr) - yql);
+    double znew = p.y;
+    if (yprev < zold) zold = yprev;
+    if (ynew < znew) znew = ynew;
+    w = ynew - znew - yprev + zold;
+    if (w > 0.0) w = 0.0;
+    w = (w > -kYCeil) ? pht_exp(w) : 0.0;
+    const double um = dev_u(ln.r);
+    xsamp = (um > w) ? xprev : p.x;
+    return 0;
+  }
+}
+
+/* ====================================================== categorical scans */
+/* start state ~ pi (oracle: orcD_pistart) */
+template <int NT>
+__device__ __forceinline__ int pistart(const Par<NT> &P, double target, int &flags) {
+  const int n = P.n();
+  double sofar = 0.0;
+  int B = 0;
+  while (sofar < target) {
+    if (B >= n) {
+      flags |= kFlagScanEnd;
+      return n - 1;
+    }
+    sofar += P.pi(B++);
+  }
+  return B - 1;
+}
+
+/* ======================================================= ECS exact path */
+template <int NT>
+struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
+  const Par<NT> &P;
+  int j;
+  double y_t, Sjj;
+  __device__ __forceinline__ double operator()(double d) const {
+    const int n = P.n();
+    const double x = y_t - d;
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; i++) acc = fma(P.W(j, i), pht_exp(P.evals(i) * x), acc);
+    return pht_log(acc) + Sjj * d;
+  }
+};
+
+template <int NT, class Env, class Sink>
+__device__ void ecs_exact(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
+  const int n = P.n();
+  double target = dev_u(ln.r);
+  const int B = pistart(P, target, ln.flags);
+  sk.start(B);
+  double t = 0.0, d;
+  int j = B, lastj;
+  for (int njump = 0;; njump++) {
+    if (njump >= kMaxJumps) {
+      ln.flags |= kFlagJumpCap;
+      break;
+    }
+    const double y_t = y - t;
+    const double Sjj = P.S(j, j);
+    if (P.s(j) > 0.0) {
+      const double U = dev_u(ln.r);
+      double den = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) den = fma(P.QQs(j, i), pht_exp(P.evals(i) * y_t), den);
+      const double pab = pht_exp(fma(Sjj, y_t, P.logs(j)) - pht_log(den));
+      if (U < pab) break;
+    }
+    lastj = j;
+    EcsDens<NT> f{P, j, y_t, Sjj};
+    double xinit[4];
+    xinit[0] = (y_t) / 1e6;
+    xinit[1] = (y_t) / 3.0;
+    xinit[2] = xinit[1] * 2.0;
+    xinit[3] = y_t - xinit[0];
+    double xsamp = 0.0;
+    const int ainfo = arms(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln);
+    if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
+    t += d = xsamp;
+    /* moveMass over candidates k (P[j,k] != 0) + categorical */
+    const double x = y_t - d;
+    double E[PHT_VEC(NT)];
+#pragma unroll
+    for (int i = 0; i < n; i++) E[i] = pht_exp(P.evals(i) * x);
+    const int cnt = P.nsuccP(j);
+    double w[PHT_VEC(NT)];
+    double sum = 0.0;
+    for (int q = 0; q < cnt; q++) {
+      const int k = P.succP(j, q);
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) acc = fma(P.QQs(k, i), E[i], acc);
+      w[q] = P.P(j, k) * acc;
+      sum += w[q];
+    }
+    target = dev_u(ln.r) * sum;
+    {
+      double sofar = 0.0;
+      int q = 0;
+      for (; q < cnt; q++) {
+        sofar += w[q];
+        if (!(sofar < target)) break;
+      }
+      if (q == cnt) {
+        ln.flags |= kFlagScanEnd;
+        q = cnt - 1;
+      }
+      j = (cnt > 0) ? P.succP(j, q) : 0;
+    }
+    sk.z(lastj, d);
+    sk.N(lastj, j);
+    ln.njump++;
+  }
+  sk.N(j, j);
+  sk.z(j, y - t);
+  sk.pre(j);
+}
+
+/* ===================================================== censored path */
+template <int NT>
+struct CjDens { /* log F_{P_j}(y - t - d) + log dexp(d; 1/-S_jj) */
+  const Par<NT> &P;
+  int j;
+  double tnow, y, scale, logscale;
+  __device__ __forceinline__ double operator()(double d) const {
+    const int n = P.n();
+    const double x1 = y - tnow - d;
+    double r1;
+    if (x1 > 0) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) acc = fma(P.V(j, i), pht_exp(P.evals(i) * x1), acc);
+      r1 = acc;
+    } else {
+      r1 = 1;
+    }
+    return pht_log(r1) + ((-d / scale) - logscale);
+  }
+};
+
+template <int NT, class Env, class Sink>
+__device__ void censored(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
+  const int n = P.n();
+  double target = dev_u(ln.r);
+  const int B = pistart(P, target, ln.flags);
+  sk.start(B);
+  double t = 0.0, lastt = 0.0;
+  int j = B, lastj = 0, njump = 0;
+  for (;;) {
+    if (njump++ >= kMaxJumps) {
+      ln.flags |= kFlagJumpCap;
+      break;
+    }
+    lastt = t;
+    lastj = j;
+    const double Sjj = P.S(j, j);
+    double d;
+    /* LJMA_condjump_r_ars */
+    if (t >= y) {
+      d = dev_rexp(ln.r, 1.0 / -Sjj);
+    } else {
+      const double x = y - t;
+      double denom = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) denom = fma(P.QQ1(j, i), pht_exp(P.evals(i) * x), denom);
+      if (t < y && dev_runif(ln.r, 0.0, 1.0) < pht_exp(Sjj * (y - t)) / denom) {
+        d = y - t + dev_rexp(ln.r, 1.0 / -Sjj);
+      } else {
+        CjDens<NT> f{P, j, t, y, P.scale(j), P.logscale(j)};
+        double xinit[4];
+        xinit[0] = (y - t) / 1e6;
+        xinit[1] = (y - t) / 3.0;
+        xinit[2] = xinit[1] * 2.0;
+        xinit[3] = y - t - xinit[0];
+        double xsamp = 0.0;
+        const int ainfo = arms(env, xinit, 0.0, y - t, f, 0.0, xsamp, ln);
+        if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
+        d = xsamp;
+      }
+    }
+    t += d;
+    target = dev_u(ln.r);
+    if (t < y) {
+      const double x1 = y - t;
+      double E[PHT_VEC(NT)];
+#pragma unroll
+      for (int i = 0; i < n; i++) E[i] = pht_exp(P.evals(i) * x1);
+      double r2 = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) r2 = fma(P.V(lastj, i), E[i], r2);
+      const int cnt = P.nsuccP(lastj);
+      const double tg = target * r2;
+      double sofar = 0.0;
+      int q = 0, sel = -1;
+      for (; q < cnt; q++) {
+        const int k = P.succP(lastj, q);
+        double r1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < n; i++) r1 = fma(P.QQ1(k, i), E[i], r1);
+        sofar += r1 * P.P(lastj, k);
+        if (!(sofar < tg)) {
+          sel = k;
+          break;
+        }
+      }
+      if (sel < 0) {
+        ln.flags |= kFlagScanEnd;
+        sel = (cnt > 0) ? P.succP(lastj, cnt - 1) : 0;
+      }
+      j = sel;
+    } else {
+      const int cnt = P.nsuccPf(lastj);
+      double sofar = 0.0;
+      int sel = -1;
+      for (int q = 0; q < cnt; q++) {
+        const int k = P.succPf(lastj, q);
+        sofar += P.Pf(lastj, k);
+        if (!(sofar < target)) {
+          sel = k;
+          break;
+        }
+      }
+      if (sel < 0) {
+        ln.flags |= kFlagScanEnd;
+        sel = (cnt > 0) ? P.succPf(lastj, cnt - 1) : 0;
+      }
+      j = sel;
+    }
+    if (j == n) break;
+    sk.z(lastj, t - lastt);
+    sk.N(lastj, j);
+    ln.njump++;
+  }
+  sk.z(lastj, t - lastt);
+  sk.pre(lastj);
+  sk.N(lastj, lastj);
+}
+
+/* ================================================================ MHRS */
+/* One LJMA_samplechain_Bladt call: returns pre; pos = stream position of
+ * the accepted attempt (replayed later for the statistics). */
+template <int NT>
+__device__ int bladt_chain(const Par<NT> &P, double y, int cens, Lane &ln, uint32_t &pos) {
+  const int n = P.n();
+  double t = 0.0;
+  int lastj = 0, natt = 0;
+  while (t < y) {
+    if (natt++ >= kMhrsMaxAtt) {
+      ln.flags |= kFlagMhrsCap;
+      break;
+    }
+    pos = pht_stream_pos(&ln.r);
+    t = 0;
+    double target = dev_u(ln.r), sofar = 0.0;
+    int B2 = 0;
+    while (sofar < target && B2 <= n) sofar += (B2 < n ? P.pi(B2) : 0.0), B2++;
+    B2--;
+    int j = B2;
+    lastj = j;
+    int njump = 0;
+    while ((t < y && j < n) || (cens && j < n)) {
+      if (njump++ >= kMaxJumps) {
+        ln.flags |= kFlagJumpCap;
+        t = y;
+        break;
+      }
+      t = t + dev_rexp(ln.r, 1.0 / -P.S(j, j));
+      target = dev_u(ln.r);
+      const int cnt = P.nsuccPf(j);
+      sofar = 0.0;
+      int sel = n + 1;
+      for (int q = 0; q < cnt; q++) {
+        const int k = P.succPf(j, q);
+        sofar += P.Pf(j, k);
+        if (!(sofar < target)) {
+          sel = k;
+          break;
+        }
+      }
+      j = sel;
+      if ((t < y && j < n) || (cens && j < n)) lastj = j;
+    }
+  }
+  return lastj;
+}
+
+template <int NT, class Sink>
+__device__ void bladt_replay(const Par<NT> &P, double y, int cens, Lane &ln, uint32_t pos, Sink &sk) {
+  const int n = P.n();
+  pht_stream r = ln.r;
+  pht_stream_seek(&r, pos);
+  double t = 0.0, lastt = 0.0, sofar = 0.0;
+  double target = pht_next_u(&r);
+  int B2 = 0;
+  while (sofar < target && B2 <= n) sofar += (B2 < n ? P.pi(B2) : 0.0), B2++;
+  B2--;
+  int j = B2, lastj = j, njump = 0;
+  sk.start(B2);
+  while ((t < y && j < n) || (cens && j < n)) {
+    if (njump++ >= kMaxJumps) {
+      t = y;
+      break;
+    }
+    {
+      const double sc = 1.0 / -P.S(j, j);
+      double e;
+      if (!isfinite(sc) || sc <= 0.0) e = (sc == 0.0) ? 0.0 : __builtin_nan("");
+      else e = sc * -pht_log(pht_next_u(&r));
+      t = t + e;
+    }
+    target = pht_next_u(&r);
+    const int cnt = P.nsuccPf(j);
+    sofar = 0.0;
+    int sel = n + 1;
+    for (int q = 0; q < cnt; q++) {
+      const int k = P.succPf(j, q);
+      sofar += P.Pf(j, k);
+      if (!(sofar < target)) {
+        sel = k;
+        break;
+      }
+    }
+    j = sel;
+    if ((t < y && j < n) || (cens && j < n)) {
+      sk.z(lastj, t - lastt);
+      sk.N(lastj, j);
+      lastj = j;
+      lastt = t;
+      ln.njump++;
+    }
+  }
+  sk.z(lastj, cens ? t - lastt : y - lastt);
+  sk.N(lastj, lastj);
+}
+
+template <int NT, class Sink>
+__device__ void mhrs(const Par<NT> &P, double y, int cens, int mhit, Lane &ln, Sink &sk) {
+  uint32_t cpos = 0, ppos = 0;
+  int cpre = bladt_chain(P, y, cens, ln, cpos);
+  while (P.s(cpre) == 0) cpre = bladt_chain(P, y, cens, ln, cpos);
+  if (cens == 0) {
+    for (int k = 0; k < mhit; k++) {
+      int ppre = bladt_chain(P, y, cens, ln, ppos);
+      while (P.s(ppre) == 0) ppre = bladt_chain(P, y, cens, ln, ppos);
+      const double U = dev_u(ln.r);
+      if (U < P.s(ppre) / P.s(cpre)) {
+        cpre = ppre;
+        cpos = ppos;
+      }
+    }
+  }
+  bladt_replay(P, y, cens, ln, cpos, sk);
+  sk.pre(cpre);
+}
+
+/* ================================================================= DCS */
+template <int NT>
+struct HobCdf {
+  const Par<NT> &P;
+  int lastj, j;
+  double prob, Pab, y, t, u, Sll, coef;
+  const double *E, *Qb;
+  __device__ __forceinline__ double operator()(double x) const {
+    const int n = P.n();
+    double tmp = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      const double ev = P.evals(i), Ei = E[i];
+      double Ji;
+      if (fabs((ev - Sll) / Sll) < 1e-13) Ji = x * Ei;
+      else Ji = (Ei - pht_exp((y - t - x) * ev + Sll * x)) / (ev - Sll);
+      tmp = fma(P.Q(j, i) * Ji, Qb[i], tmp);
+    }
+    return 1 / prob * P.S(lastj, j) / Pab * tmp - u;
+  }
+};
+
+template <class F>
+__device__ double find02(double ax, double bx, double fa, double fb, const F &f, double *Tol, int *Maxit,
+                         int &nevals) {
+  double a, b, c, fc, tol;
+  int maxit;
+  a = ax; b = bx;
+  c = a; fc = fa;
+  maxit = *Maxit + 1; tol = *Tol;
+  if (fa == 0.0) { *Tol = 0.0; *Maxit = 0; return a; }
+  if (fb == 0.0) { *Tol = 0.0; *Maxit = 0; return b; }
+  while (maxit--) {
+    double prev_step = b - a, tol_act, p, q, new_step;
+    if (fabs(fc) < fabs(fb)) {
+      a = b; b = c; c = a;
+      fa = fb; fb = fc; fc = fa;
+    }
+    tol_act = 2 * 2.2204460492503131e-16 * fabs(b) + tol / 2;
+    new_step = (c - b) / 2;
+    if (fabs(new_step) <= tol_act || fb == (double)0) {
+      *Maxit -= maxit;
+      *Tol = fabs(c - b);
+      return b;
+    }
+    if (fabs(prev_step) >= tol_act && fabs(fa) > fabs(fb)) {
+      double t1, cb, t2;
+      cb = c - b;
+      if (a == c) {
+        t1 = fb / fa;
+        p = cb * t1;
+        q = 1.0 - t1;
+      } else {
+        q = fa / fc; t1 = fb / fc; t2 = fb / fa;
+        p = t2 * (cb * q * (q - t1) - (b - a) * (t1 - 1.0));
+        q = (q - 1.0) * (t1 - 1.0) * (t2 - 1.0);
+      }
+      if (p > (double)0) q = -q;
+      else p = -p;
+      if (p < (0.75 * cb * q - fabs(tol_act * q) / 2) && p < fabs(prev_step * q / 2)) new_step = p / q;
+    }
+    if (fabs(new_step) < tol_act) new_step = (new_step > (double)0) ? tol_act : -tol_act;
+    a = b; fa = fb;
+    b += new_step; fb = f(b);
+    nevals++;
+    if ((fb > 0 && fc > 0) || (fb < 0 && fc < 0)) { c = a; fc = fa; }
+  }
+  *Tol = fabs(c - b);
+  *Maxit = -1;
+  return b;
+}
+
+template <int NT, class Sink>
+__device__ void dcs(const Par<NT> &P, double y, Lane &ln, Sink &sk) {
+  const int n = P.n();
+  /* end state b ~ (pi e^{yS})_b s_b */
+  double a[PHT_VEC(NT)];
+#pragma unroll
+  for (int i = 0; i < n; i++) a[i] = P.piQ(i) * pht_exp(P.evals(i) * y);
+  int b;
+  {
+    double pend[PHT_VEC(NT)], sum = 0.0;
+#pragma unroll
+    for (int k = 0; k < n; k++) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) acc = fma(a[i], P.Qinv(i, k), acc);
+      pend[k] = acc * P.s(k);
+      sum += pend[k];
+    }
+    const double tg = dev_u(ln.r) * sum;
+    double sofar = 0.0;
+    int q = 0;
+    for (; q < n; q++) {
+      sofar += pend[q];
+      if (!(sofar < tg)) break;
+    }
+    if (q == n) {
+      ln.flags |= kFlagScanEnd;
+      q = n - 1;
+    }
+    b = q;
+  }
+  double Qb[PHT_VEC(NT)];
+#pragma unroll
+  for (int i = 0; i < n; i++) Qb[i] = P.Qinv(i, b);
+  double target = dev_u(ln.r);
+  const int B = pistart(P, target, ln.flags);
+  sk.start(B);
+  double t = 0.0, jtime = 0.0;
+  int j = B, lastj, njump = 0;
+  while (t < y) {
+    if (njump++ >= kMaxJumps) {
+      ln.flags |= kFlagJumpCap;
+      break;
+    }
+    lastj = j;
+    const double x = y - t;
+    const double Sjj = P.S(j, j);
+    double E[PHT_VEC(NT)];
+#pragma unroll
+    for (int i = 0; i < n; i++) E[i] = pht_exp(P.evals(i) * x);
+    double Pab = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; i++) Pab = fma(P.Q(j, i) * E[i], Qb[i], Pab);
+    if (j == b) {
+      if (dev_runif(ln.r, 0.0, 1.0) < pht_exp(Sjj * (y - t)) / Pab) {
+        sk.z(j, (y - t));
+        sk.N(j, j);
+        sk.pre(j);
+        return;
+      }
+    }
+    double J[PHT_VEC(NT)];
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      const double ev = P.evals(i);
+      if (fabs((ev - Sjj) / Sjj) < 1e-13) J[i] = x * E[i];
+      else J[i] = (E[i] - pht_exp(Sjj * x)) / (ev - Sjj);
+    }
+    const int cnt = P.nsuccS(j);
+    double pw[PHT_VEC(NT)];
+    double p_sum = 0.0;
+    for (int q = 0; q < cnt; q++) {
+      const int i = P.succS(j, q);
+      double tmp = 0.0;
+#pragma unroll
+      for (int k = 0; k < n; k++) tmp = fma(P.Q(i, k) * J[k], Qb[k], tmp);
+      p_sum += pw[q] = P.S(j, i) / Pab * tmp;
+    }
+    target = dev_runif(ln.r, 0.0, p_sum);
+    if (!(target > 0.0)) {
+      ln.flags |= kFlagDcsZero;
+      sk.pre(j);
+      return;
+    }
+    double prob;
+    {
+      double sofar = 0.0;
+      int q = 0;
+      for (; q < cnt; q++) {
+        sofar += pw[q];
+        if (!(sofar < target)) break;
+      }
+      if (q == cnt) {
+        ln.flags |= kFlagScanEnd;
+        q = cnt - 1;
+      }
+      j = P.succS(j, q);
+      prob = pw[q];
+    }
+    HobCdf<NT> hc{P, lastj, j, prob, Pab, y, t, 0.0, Sjj, 0.0, E, Qb};
+    hc.u = dev_runif(ln.r, 0.0, 1.0);
+    double Tol = 0.0;
+    int Maxit = 1000;
+    jtime = find02(0.0, y - t, -hc.u, 1.0 - hc.u, hc, &Tol, &Maxit, ln.nbrent);
+    while (t + jtime >= y) jtime = jtime / 2;
+    sk.N(lastj, j);
+    sk.z(lastj, jtime);
+    t += jtime;
+    ln.njump++;
+  }
+}
+
+}  // namespace pht
+#endif

@@ -1,0 +1,40 @@
+/*
+ * pht_kernels.h — host/device interface of the sweep kernels.
+ */
+#ifndef PHT_KERNELS_H
+#define PHT_KERNELS_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pht {
+
+constexpr int kBlock = 256;
+/* method bitmask values of LJMA_Gibbs (src/PHT_MCMC_Aslett.c:69-71) */
+constexpr int kMethodMHRS = 0x1;
+constexpr int kMethodECS = 0x2;
+constexpr int kMethodDCS = 0x4;
+
+struct SweepArgs {
+  const unsigned char *params; /* packed block (pht_layout.h), device */
+  int n;
+  int mhit;
+  long count;                  /* observations in this launch */
+  const double *y;             /* [count] */
+  const int *cens;             /* [count] */
+  const uint32_t *gid;         /* [count] global observation index (Philox counter) */
+  uint32_t k0, k1, sweep;
+  double zscale;               /* 2^zexp */
+  unsigned long long *stats;   /* [stats_len(n)] int64, accumulated */
+  /* debug per-observation outputs (DEBUG kernels only) */
+  long long *dbg_zq;           /* [count*n] */
+  int *dbg_N;                  /* [count*n*n] */
+  int *dbg_B, *dbg_pre, *dbg_flags;
+  uint32_t *dbg_ndraw;
+};
+
+}  // namespace pht
+
+extern "C" hipError_t pht_launch_sweep(const pht::SweepArgs *a, int method, int debug, hipStream_t st);
+
+#endif

@@ -1,0 +1,170 @@
+/*
+ * pht_kernels.hip — the Gibbs "step 1" sweep kernels for gfx950.
+ *
+ * One lane = one observation (SURVEY.md §8e sharding).  A workgroup stages
+ * the packed per-sweep parameter block (pht_layout.h) into LDS once, each
+ * lane runs its observation's latent-path sampler (pht_device.h) and adds
+ * its sufficient statistics into workgroup-level integer accumulators in
+ * LDS (z as int64 fixed point, counts as u32), which are flushed to the
+ * global int64 statistics block with integer atomics.  Integer sums are
+ * order-independent, so the result is bit-identical for any grid, any
+ * workgroup schedule and any number of GPUs.
+ *
+ * Replaces, per sweep: LJMA_MHsample_Bladt / LJMA_MHsample_Aslett2 /
+ * LJMA_MHsample_Hobolth2 (src/PHT_MCMC_Aslett.c:325-333).
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pht_device.h"
+#include "pht_env.h"
+#include "pht_kernels.h"
+
+namespace pht {
+
+/* Statistics sink: workgroup accumulators in LDS (+ per-observation debug
+ * rows in global memory when DEBUG). */
+template <bool DEBUG>
+struct Sink {
+  unsigned long long *zq; /* LDS [n] */
+  unsigned *Bc;           /* LDS [n] */
+  unsigned *Nc;           /* LDS [n*n] */
+  int n;
+  double zscale;
+  long long *dz;          /* debug row [n] */
+  int *dN;                /* debug row [n*n] */
+  int *dB, *dpre;
+  __device__ __forceinline__ void z(int k, double d) {
+    const long long q = (long long)rint(d * zscale);
+    atomicAdd(&zq[k], (unsigned long long)q);
+    if (DEBUG) dz[k] += q;
+  }
+  __device__ __forceinline__ void N(int i, int j) {
+    atomicAdd(&Nc[i + j * n], 1u);
+    if (DEBUG) dN[i + j * n] += 1;
+  }
+  __device__ __forceinline__ void start(int b) {
+    atomicAdd(&Bc[b], 1u);
+    if (DEBUG) *dB = b;
+  }
+  __device__ __forceinline__ void pre(int j) {
+    if (DEBUG) *dpre = j;
+  }
+};
+
+template <int NT>
+__device__ __forceinline__ int nval(int n) { return NT > 0 ? NT : n; }
+
+template <int NT, int METHOD, bool DEBUG, class Env>
+__device__ __forceinline__ void sweep_body(const SweepArgs &a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int n = nval<NT>(a.n);
+  const Layout L = make_layout(n);
+  const int pbytes = L.bytes();
+  /* stage the parameter block */
+  {
+    const int4 *src = reinterpret_cast<const int4 *>(a.params);
+    int4 *dst = reinterpret_cast<int4 *>(smem);
+    for (int k = threadIdx.x; k < pbytes / 16; k += blockDim.x) dst[k] = src[k];
+  }
+  unsigned long long *zq = reinterpret_cast<unsigned long long *>(smem + pbytes);
+  unsigned long long *xc = zq + n; /* kStatExtra counters */
+  unsigned *Bc = reinterpret_cast<unsigned *>(xc + kStatExtra);
+  unsigned *Nc = Bc + n;
+  for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
+  for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
+  __syncthreads();
+
+  Par<NT> P;
+  P.d = reinterpret_cast<const double *>(smem);
+  P.iv = reinterpret_cast<const int *>(smem + L.ndouble * 8);
+  P.L = L;
+
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < a.count) {
+    Lane ln;
+    pht_stream_init(&ln.r, a.k0, a.k1, a.gid[i], 0u, a.sweep);
+    ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
+    Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
+    if (DEBUG) {
+      sk.dz = a.dbg_zq + i * n;
+      sk.dN = a.dbg_N + i * n * n;
+      sk.dB = a.dbg_B + i;
+      sk.dpre = a.dbg_pre + i;
+    }
+    const double y = a.y[i];
+    Env env;
+    env.bind(threadIdx.x);
+    if (METHOD == kMethodMHRS) {
+      mhrs<NT>(P, y, a.cens[i], a.mhit, ln, sk);
+    } else if (METHOD == kMethodDCS) {
+      dcs<NT>(P, y, ln, sk);
+    } else {
+      if (a.cens[i]) censored<NT>(P, y, ln, env, sk);
+      else ecs_exact<NT>(P, y, ln, env, sk);
+    }
+    const uint32_t nd = pht_stream_pos(&ln.r);
+    if (DEBUG) {
+      a.dbg_flags[i] = ln.flags;
+      a.dbg_ndraw[i] = nd;
+    }
+    atomicAdd(&xc[0], 1ull);
+    atomicAdd(&xc[1], (unsigned long long)ln.neval);
+    if (ln.flags) atomicAdd(&xc[2], 1ull);
+    atomicAdd(&xc[3], (unsigned long long)nd);
+    atomicAdd(&xc[4], (unsigned long long)ln.njump);
+    atomicAdd(&xc[5], (unsigned long long)ln.nbrent);
+  }
+  __syncthreads();
+  /* flush: [zq n][B n][N n*n][extra] */
+  unsigned long long *g = a.stats;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    if (zq[k]) atomicAdd(&g[k], zq[k]);
+    if (Bc[k]) atomicAdd(&g[n + k], (unsigned long long)Bc[k]);
+  }
+  for (int k = threadIdx.x; k < n * n; k += blockDim.x)
+    if (Nc[k]) atomicAdd(&g[2 * n + k], (unsigned long long)Nc[k]);
+  for (int k = threadIdx.x; k < kStatExtra; k += blockDim.x)
+    if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
+}
+
+template <int NT, int METHOD, bool DEBUG>
+__global__ void __launch_bounds__(kBlock) sweep_kernel(SweepArgs a) {
+  sweep_body<NT, METHOD, DEBUG, EnvPrivate>(a);
+}
+
+/* LDS bytes a workgroup needs: parameter block + accumulators */
+static int smem_bytes(int n) {
+  const Layout L = make_layout(n);
+  return L.bytes() + (n + kStatExtra) * 8 + (n + n * n) * 4;
+}
+
+template <int NT>
+static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStream_t st) {
+  const int blocks = (int)((a.count + kBlock - 1) / kBlock);
+  if (blocks == 0) return hipSuccess;
+  const int sm = smem_bytes(a.n);
+#define PHT_LAUNCH(M, D) hipLaunchKernelGGL((sweep_kernel<NT, M, D>), dim3(blocks), dim3(kBlock), sm, st, a)
+  if (method == kMethodMHRS) {
+    if (debug) PHT_LAUNCH(kMethodMHRS, true); else PHT_LAUNCH(kMethodMHRS, false);
+  } else if (method == kMethodDCS) {
+    if (debug) PHT_LAUNCH(kMethodDCS, true); else PHT_LAUNCH(kMethodDCS, false);
+  } else {
+    if (debug) PHT_LAUNCH(kMethodECS, true); else PHT_LAUNCH(kMethodECS, false);
+  }
+#undef PHT_LAUNCH
+  return hipGetLastError();
+}
+
+}  // namespace pht
+
+extern "C" hipError_t pht_launch_sweep(const pht::SweepArgs *a, int method, int debug, hipStream_t st) {
+  using namespace pht;
+  if (a->n < 1 || a->n > kMaxN) return hipErrorInvalidValue;
+  if ((make_layout(a->n).bytes() & 15) != 0) return hipErrorInvalidValue;
+  switch (a->n) {
+    case 3: return launch_nt<3>(*a, method, debug != 0, st);
+    case 10: return launch_nt<10>(*a, method, debug != 0, st);
+    default: return launch_nt<0>(*a, method, debug != 0, st);
+  }
+}

@@ -1,0 +1,129 @@
+"""GPU parity: the HIP kernels against the oracle's device-spec restatement
+(oracle/pht_oracle_impl.h, ORC_DEV), bit for bit, per observation.
+
+Bar: B, pre-absorption state, flags, uniforms consumed, fixed-point z and
+the transition counts N are *identical* for every observation; the int64
+statistics block is identical.  Sizes are those the CPU oracle finishes in
+seconds.  Also: sharding invariance, full Gibbs chains bit-exact against the
+oracle's device-variant LJMA_Gibbs, and statistical agreement with the
+reference's own C (kernel vs oracle/_ref)."""
+import numpy as np
+import pytest
+
+import phasetype_amd as P
+from phasetype_amd.synth import bd_exit, bd_exit_structure, simulate_ph
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # (n, N, censor_frac, method, mhit)
+    (3, 3000, 0.0, 2, 1), (3, 3000, 0.3, 2, 1), (3, 2000, 0.3, 1, 1), (3, 2000, 0.0, 1, 4), (3, 2000, 0.0, 4, 1),
+    (5, 2000, 0.3, 2, 1), (5, 1000, 0.3, 1, 2), (5, 1500, 0.3, 4, 1),
+    (10, 2000, 0.3, 2, 1), (10, 1000, 0.3, 1, 1), (10, 1000, 0.0, 4, 1),
+    (15, 600, 0.3, 2, 1), (15, 300, 0.3, 1, 1), (15, 300, 0.3, 4, 1),
+]
+
+
+def _perturbed(n, seed):
+    S, s = bd_exit(n)
+    rng = np.random.default_rng(seed)
+    S = S.copy()
+    mask = (S > 0)
+    S[mask] *= rng.uniform(0.7, 1.3, mask.sum())
+    s = s * rng.uniform(0.7, 1.3, n)
+    np.fill_diagonal(S, 0.0)
+    np.fill_diagonal(S, -(S.sum(1) + s))
+    return S, s
+
+
+@pytest.mark.parametrize("n,N,cf,method,mhit", CASES)
+def test_per_observation_bitexact(gpu, orc, n, N, cf, method, mhit):
+    S0, s0 = bd_exit(n)
+    y, cen = simulate_ph(S0, s0, N, seed=1000 + n, censor_frac=cf)
+    S, s = _perturbed(n, n)
+    key, sweep = (0x1234567 + n, 0x89ABCDE), 7
+    zexp = int(orc.lib.orc_zexp(np.ascontiguousarray(y), len(y)))
+    o = orc.dev_sweep(method, S, s, y, cen, mhit=mhit, key=key, sweep=sweep, zexp=zexp)
+    sw = P.Sweeper(n, method, mhit)
+    sw.set_obs(y, cen)
+    g = sw.sweep_debug(S, s, key=key, sweep=sweep, zexp=zexp)
+    for f in ("B", "pre", "flags", "ndraw"):
+        bad = np.nonzero(g[f] != o[f])[0]
+        assert bad.size == 0, f"{f} differs at obs {bad[:5]}: gpu {g[f][bad[:5]]} oracle {o[f][bad[:5]]}"
+    bad = np.nonzero(np.any(g["zq"] != o["zq"], axis=1))[0]
+    assert bad.size == 0, f"zq differs at obs {bad[:5]}"
+    bad = np.nonzero(np.any(g["N"] != o["N"], axis=(1, 2)))[0]
+    assert bad.size == 0, f"N differs at obs {bad[:5]}"
+    zq, B, Nt, ex = P.split_stats(g["stats"], n)
+    assert np.array_equal(zq, o["zq_tot"])
+    assert np.array_equal(B, o["B_tot"])
+    assert np.array_equal(Nt, o["N_tot"])
+    assert ex[0] == N
+    # the non-debug kernel produces the same block
+    st = sw.sweep(S, s, key=key, sweep=sweep, zexp=zexp)
+    assert np.array_equal(st[:2 * n + n * n], g["stats"][:2 * n + n * n])
+
+
+@pytest.mark.parametrize("method", [1, 2, 4])
+def test_shard_invariance(gpu, method):
+    """Two shards (obs0 offsets) sum to the single-shard block exactly."""
+    n, N = 6, 4000
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, N, seed=77, censor_frac=0.3)
+    zexp = P.zexp_for(y)
+    full = P.Sweeper(n, method)
+    full.set_obs(y, cen)
+    a = full.sweep(S, s, key=(5, 6), sweep=3, zexp=zexp)
+    parts = []
+    for lo, hi in ((0, 1234), (1234, N)):
+        sw = P.Sweeper(n, method)
+        sw.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
+        parts.append(sw.sweep(S, s, key=(5, 6), sweep=3, zexp=zexp))
+    k = 2 * n + n * n
+    assert np.array_equal(a[:k], parts[0][:k] + parts[1][:k])
+
+
+@pytest.mark.parametrize("method,n", [(2, 4), (1, 4), (4, 4), (2, 10)])
+def test_gibbs_chain_bitexact(gpu, orc, method, n):
+    """pht_gibbs_run (GPU step 1 + host Gamma update) == oracle device-variant
+    LJMA_Gibbs, every draw of every iteration."""
+    T, theta = bd_exit_structure(n)
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 1500, seed=5, censor_frac=0.3 if method != 4 else 0.0)
+    m = len(theta)
+    nu, zeta = 1 + 50 * theta, np.full(m, 50.0)
+    it = 12
+    Cm = np.ones_like(T, dtype=np.float64)
+    orc.set_seed(2024)
+    want = orc.gibbs(1, it, 1, method, n, nu, zeta, T.reshape(-1, order="F"), Cm.reshape(-1, order="F"), y, cen)
+    P.set_seed(2024)
+    sw = P.Sweeper(n, method, 1)
+    sw.set_obs(y, cen)
+    got = sw.gibbs(it, method, nu, zeta, T, Cm, P.zexp_for(y))
+    assert np.array_equal(got, want), np.abs(got - want).max()
+    # the .C entry point over all GPUs gives the same chain
+    P.set_seed(2024)
+    out = P.LJMA_Gibbs(it, 1, method, n, m, nu, zeta, T, Cm, y, len(y), cen, [-1.0], 1, np.zeros(it * m))
+    assert np.array_equal(out["res"].reshape(m, it).T, want)
+
+
+def test_statistical_vs_reference(gpu, ref):
+    """GPU step 1 vs the reference's own C on identical (S, s, y): sufficient
+    statistics agree within Monte-Carlo error (different random streams)."""
+    n, N = 4, 20000
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, N, seed=11, censor_frac=0.3)
+    for method in (1, 2, 4):
+        ref.set_seed(99)
+        Br, zr, Nr = ref.sweep(method, S, s, y, cen, per_obs=True)
+        sw = P.Sweeper(n, method)
+        sw.set_obs(y, cen)
+        zexp = P.zexp_for(y)
+        g = sw.sweep_debug(S, s, key=(3, 4), sweep=1, zexp=zexp)
+        zg = g["zq"] * 2.0 ** -zexp
+        for k in range(n):
+            se = np.sqrt(zr[:, k].var() / N + zg[:, k].var() / N)
+            assert abs(zr[:, k].mean() - zg[:, k].mean()) < 5 * se + 1e-12, (method, k)
+        ng, nr = g["N"].reshape(N, -1).astype(float), Nr.reshape(N, -1).astype(float)
+        se = np.sqrt(nr.var(0) / N + ng.var(0) / N) + 1e-12
+        assert np.all(np.abs(nr.mean(0) - ng.mean(0)) < 5 * se + 1e-9), method
