@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""bench.py — Gibbs iterations/s of the PhaseType hot path on MI355X.
+
+Workload (BASELINE.json metric, configs[3] "cfg4"): phtMCMC2's default ECS
+sampler on the BD-exit(n=10) generator (m = 28 parameters), N = 1e6 exact
+synthetic absorption times; one *step* = one full Gibbs sweep = host
+per-sweep spectral setup (P/Pfull, dgeevx, Q^-1 v, packed parameters) +
+step-1 latent-path sampling of every observation on the GPU(s) + the
+sufficient-statistics reduction + the host conjugate Gamma update
+(src/PHT_MCMC_Aslett.c:268-405).  Nothing is skipped inside the timed
+region; observations are resident in HBM before timing starts.
+
+Multi-GPU (strong scaling, N fixed): one process per GPU, rank r owns a
+contiguous shard of the observations; each sweep's int64 statistics block is
+summed across ranks with one all-reduce (torch.distributed, backend "nccl" =
+RCCL over xGMI) and every rank draws the identical Gamma update.
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for the
+roofline and cpu_baseline fields).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import phasetype_amd as P  # noqa: E402
+from phasetype_amd.synth import DATA_KEY, bd_exit, bd_exit_structure, simulate_ph  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
+FP64_VALU_PEAK_TF = 78.6  # MI355X FP64 vector peak (spec)
+ALG_BYTES_PER_OBS = 12    # y f64 + censored i32 per observation per sweep
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(n, y, cen, T, nu, zeta, target_s=15.0):
+    """The reference's own C (oracle/_ref/libpht_ref.so, compiled in place from
+    /root/reference/src) timed single-threaded on a bounded sample of the same
+    workload; falls back to the bit-exact restatement (oracle ref variant)."""
+    from oracle import oracle as O
+
+    kind = "reference"
+    try:
+        lib = O.RefLib()
+        run = lambda it, yy, cc: lib.gibbs(it, 1, 2, n, nu, zeta, T.reshape(-1, order="F"),  # noqa: E731
+                                           np.ones(T.size), yy, cc)
+    except Exception as e:  # noqa: BLE001
+        log(f"[bench] reference oracle unavailable ({e}); timing the restatement")
+        kind = "port"
+        lib = O.OracleLib()
+        run = lambda it, yy, cc: lib.gibbs(0, it, 1, 2, n, nu, zeta, T.reshape(-1, order="F"),  # noqa: E731
+                                           np.ones(T.size), yy, cc)
+    lib.set_seed(1)
+    probe = 20000
+    t0 = time.perf_counter()
+    run(2, y[:probe], cen[:probe])
+    per_obs_sweep = (time.perf_counter() - t0) / probe
+    nsamp = int(min(len(y), max(20000, 200000)))
+    sweeps = max(2, int(target_s / max(per_obs_sweep * nsamp, 1e-9)))
+    sweeps = min(sweeps, 50)
+    lib.set_seed(2)
+    t0 = time.perf_counter()
+    run(sweeps + 1, y[:nsamp], cen[:nsamp])
+    dt = time.perf_counter() - t0
+    rate_sample = sweeps / dt
+    value = rate_sample * nsamp / len(y)  # sweeps/s scaled to the full N (work is linear in N)
+    return {"value": value, "unit": "iterations/s", "cores": 1, "kind": kind,
+            "sample": f"{sweeps} Gibbs sweeps over the first {nsamp} of the {len(y)} observations "
+                      f"({dt:.1f} s, {rate_sample:.4f} sweeps/s), scaled by {nsamp}/{len(y)} to N={len(y)}; "
+                      f"single thread of the GPU box's host CPU"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=10)
+    ap.add_argument("--N", type=int, default=1_000_000)
+    ap.add_argument("--method", default="ECS", choices=["ECS", "MHRS", "DCS"])
+    ap.add_argument("--censor", type=float, default=0.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_latest.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    n, N = args.n, args.N
+    method = P.METHODS[args.method]
+    S, s = bd_exit(n)
+    T, theta = bd_exit_structure(n)
+    m = len(theta)
+    nu, zeta = 1.0 + 50.0 * theta, np.full(m, 50.0)
+    y, cen = simulate_ph(S, s, N, seed=DATA_KEY, censor_frac=args.censor)
+    zexp = P.zexp_for(y)
+    lo, hi = N * rank // world, N * (rank + 1) // world
+    sw = P.Sweeper(n, method, 1, device=local)
+    sw.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
+    Cm = np.ones(T.shape)
+
+    reduce = None
+    if dist is not None:
+        import torch
+
+        buf = torch.zeros(P.stats_len(n), dtype=torch.int64, device=f"cuda:{local}")
+
+        def reduce(arr):  # noqa: F811
+            buf.copy_(torch.from_numpy(arr))
+            dist.all_reduce(buf)
+            arr[:] = buf.cpu().numpy()
+
+    def sync():
+        if dist is not None:
+            import torch
+
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    P.set_seed(20241008)
+    warm = sw.gibbs(args.warmup + 1, method, nu, zeta, T, Cm, zexp, reduce=reduce)
+    start = warm[-1]
+    sync()
+    t0 = time.perf_counter()
+    res = sw.gibbs(args.steps + 1, method, nu, zeta, T, Cm, zexp, start=start, reduce=reduce)
+    sync()
+    dt = time.perf_counter() - t0
+    kernel_ms = sw.kernel_ms_total / args.steps
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([dt, kernel_ms], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, kernel_ms = float(t[0]), float(t[1])
+    if not np.all(np.isfinite(res)):
+        raise SystemExit("non-finite Gibbs draws")
+
+    if rank == 0:
+        sweeps_per_s = args.steps / dt
+        local_obs = hi - lo
+        achieved = ALG_BYTES_PER_OBS * local_obs / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_file):
+            try:
+                tf = json.load(open(args.traffic_file))
+                if tf.get("n") == n and tf.get("N_local") == local_obs and tf.get("method") == args.method:
+                    traffic = tf.get("hbm_bytes_per_launch")
+            except Exception:  # noqa: BLE001
+                traffic = None
+        line = {
+            "metric": "Gibbs iterations/sec (whole node), n=10 states × N=1e6 observations",
+            "value": sweeps_per_s,
+            "unit": "iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": f"synthetic: N={N} absorption times simulated from BD-exit(n={n}) (pi=e1), "
+                    f"censored fraction {args.censor}, Philox key 0x{DATA_KEY:x}",
+            "config": {"workload": f"cfg4: phtMCMC2 {args.method}, n={n} states, m={m} parameters, "
+                                   f"N={N} exact obs, priors nu=1+50*theta, zeta=50, mhit=1",
+                       "n": n, "N": N, "method": args.method, "parallelism": f"obs-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel_ms": kernel_ms,
+                         "note": f"sweep kernel, {ALG_BYTES_PER_OBS} B/obs x {local_obs} obs per launch / "
+                                 "HIP-event kernel time; the path is FP64-VALU/latency bound, see roofline_valu"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(n, y, cen, T, nu, zeta)
+            except Exception as e:  # noqa: BLE001
+                log(f"[bench] cpu baseline failed: {e}")
+                line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -72,7 +72,7 @@ def load(build_if_needed: bool = True) -> C.CDLL:
         _build.build()
     if not os.path.exists(_build.LIB):
         raise PhaseTypeError(f"native library missing: {_build.LIB} (run phasetype_amd/build.py)")
-    L = C.CDLL(_build.LIB, mode=C.RTLD_GLOBAL)
+    L = C.CDLL(_build.LIB, mode=C.RTLD_LOCAL)
     L.pht_last_error.restype = C.c_char_p
     L.pht_bind_lapack.argtypes = [C.c_char_p, C.c_char_p]
     L.pht_set_seed.argtypes = [C.c_uint32]

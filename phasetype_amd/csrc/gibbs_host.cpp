@@ -307,6 +307,7 @@ struct pht_ctx {
   hipStream_t stream = nullptr;
   int n = 0, method = 0, mhit = 1;
   long count = 0;
+  long n_exact = 0;                      /* observations [0, n_exact) are exact (sorted first) */
   double *d_y = nullptr;
   int *d_cens = nullptr;
   uint32_t *d_gid = nullptr;
@@ -425,6 +426,8 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
     cs[k] = cens[ord[k]];
     gs[k] = (uint32_t)(obs0 + ord[k]);
   }
+  c->n_exact = 0;
+  while (c->n_exact < count && cs[c->n_exact] == 0) c->n_exact++;
   c->order = std::move(ord);
   HIPCHK(hipMalloc(&c->d_y, sizeof(double) * count));
   HIPCHK(hipMalloc(&c->d_cens, sizeof(int) * count));
@@ -479,7 +482,20 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     a.dbg_ndraw = c->d_ndraw;
   }
   HIPCHK(hipEventRecord(c->ev0, c->stream));
-  HIPCHK(pht_launch_sweep(&a, c->method, debug ? 1 : 0, c->stream));
+  if (c->method == kMethodECS) {
+    /* exact observations: persistent ECS kernel; censored: LJMA_samplechain path */
+    SweepArgs ae = a;
+    ae.begin = 0;
+    ae.count = c->n_exact;
+    ae.cens = nullptr;
+    if (ae.count > 0) HIPCHK(pht_launch_sweep(&ae, c->method, debug ? 1 : 0, c->stream));
+    SweepArgs ac = a;
+    ac.begin = c->n_exact;
+    ac.count = c->count - c->n_exact;
+    if (ac.count > 0) HIPCHK(pht_launch_sweep(&ac, c->method, debug ? 1 : 0, c->stream));
+  } else {
+    HIPCHK(pht_launch_sweep(&a, c->method, debug ? 1 : 0, c->stream));
+  }
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   HIPCHK(hipMemcpyAsync(c->h_stats, c->d_stats, sizeof(unsigned long long) * sl, hipMemcpyDeviceToHost, c->stream));
   return 0;
@@ -723,7 +739,7 @@ extern "C" void LJMA_Gibbs(int *it, int *mhit, int *method, int *n, int *m, doub
   std::vector<pht_ctx *> ctxs;
   int rc = 0;
   if (ndev <= 0) {
-    set_err("PhaseType (MI355X): no HIP device available");
+    set_err("no HIP device available");
     rc = -1;
   }
   const long L = *l;

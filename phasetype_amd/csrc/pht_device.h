@@ -101,7 +101,10 @@ struct Lane {
 };
 
 /* ===================================================================== ARMS */
-template <class Env>
+/* Envelope policies (pht_env.h) expose X/Y/CUM getters and sX/sY/sCUM
+ * setters; ey = expshift(y, ymax) is recomputed where needed instead of
+ * stored (the reference stores it, src/arms.c:19; recomputation from the
+ * same y and ymax is bit-identical). */
 __device__ __forceinline__ double expshift(double y, double y0) {
   return (y - y0 > -2.0 * kYCeil) ? pht_exp(y - y0 + kYCeil) : 0.0;
 }
@@ -112,33 +115,35 @@ __device__ void arms_meet(Env &e, int k) {
   double gl = 0.0, gr = 0.0, grl = 0.0, dl = 0.0, dr = 0.0;
   const int last = e.cnt - 1;
   const bool il = (k >= 3), ir = (k + 3 <= last), irl = (k >= 1 && k + 1 <= last);
-  if (il) gl = (e.Y(k - 1) - e.Y(k - 3)) / (e.X(k - 1) - e.X(k - 3));
-  if (ir) gr = (e.Y(k + 1) - e.Y(k + 3)) / (e.X(k + 1) - e.X(k + 3));
-  if (irl) grl = (e.Y(k + 1) - e.Y(k - 1)) / (e.X(k + 1) - e.X(k - 1));
+  double xm1 = 0.0, ym1 = 0.0, xp1 = 0.0, yp1 = 0.0;
+  if (k >= 1) { xm1 = e.X(k - 1); ym1 = e.Y(k - 1); }
+  if (k + 1 <= last) { xp1 = e.X(k + 1); yp1 = e.Y(k + 1); }
+  if (il) gl = (ym1 - e.Y(k - 3)) / (xm1 - e.X(k - 3));
+  if (ir) gr = (yp1 - e.Y(k + 3)) / (xp1 - e.X(k + 3));
+  if (irl) grl = (yp1 - ym1) / (xp1 - xm1);
   if (irl && il && (gl < grl)) gl = gl + (1.0 + 1.0) * (grl - gl);
   if (irl && ir && (gr > grl)) gr = gr + (1.0 + 1.0) * (grl - gr);
   if (il && irl) {
-    dr = (gl - grl) * (e.X(k + 1) - e.X(k - 1));
+    dr = (gl - grl) * (xp1 - xm1);
     if (dr < kYEps) dr = kYEps;
   }
   if (ir && irl) {
-    dl = (grl - gr) * (e.X(k + 1) - e.X(k - 1));
+    dl = (grl - gr) * (xp1 - xm1);
     if (dl < kYEps) dl = kYEps;
   }
   if (il && ir && irl) {
-    const double xr = e.X(k + 1), xl = e.X(k - 1), yr = e.Y(k + 1), yl = e.Y(k - 1);
-    e.X(k) = (dl * xr + dr * xl) / (dl + dr);
-    e.Y(k) = (dl * yr + dr * yl + dl * dr) / (dl + dr);
+    e.sX(k, (dl * xp1 + dr * xm1) / (dl + dr));
+    e.sY(k, (dl * yp1 + dr * ym1 + dl * dr) / (dl + dr));
   } else if (il && irl) {
-    e.X(k) = e.X(k + 1);
-    e.Y(k) = e.Y(k + 1) + dr;
+    e.sX(k, xp1);
+    e.sY(k, yp1 + dr);
   } else if (ir && irl) {
-    e.X(k) = e.X(k - 1);
-    e.Y(k) = e.Y(k - 1) + dl;
+    e.sX(k, xm1);
+    e.sY(k, ym1 + dl);
   } else if (il) {
-    e.Y(k) = e.Y(k - 1) + gl * (e.X(k) - e.X(k - 1));
+    e.sY(k, ym1 + gl * (e.X(k) - xm1));
   } else if (ir) {
-    e.Y(k) = e.Y(k + 1) - gr * (e.X(k + 1) - e.X(k));
+    e.sY(k, yp1 - gr * (xp1 - e.X(k)));
   }
 }
 
@@ -150,20 +155,19 @@ __device__ void arms_cumulate(Env &e) {
     if (yk > ymax) ymax = yk;
   }
   e.ymax = ymax;
-  double eyp = expshift<Env>(e.Y(0), ymax), xp = e.X(0), yp = e.Y(0);
-  e.EY(0) = eyp;
+  double xp = e.X(0), yp = e.Y(0);
+  double eyp = expshift(yp, ymax);
   double cum = 0.;
-  e.CUM(0) = cum;
+  e.sCUM(0, cum);
   for (int k = 1; k < e.cnt; k++) {
     const double xk = e.X(k), yk = e.Y(k);
-    const double eyk = expshift<Env>(yk, ymax);
-    e.EY(k) = eyk;
+    const double eyk = expshift(yk, ymax);
     double a;
     if (xp == xk) a = 0.;
     else if (fabs(yk - yp) < kYEps) a = 0.5 * (eyk + eyp) * (xk - xp);
     else a = ((eyk - eyp) / (yk - yp)) * (xk - xp);
     cum = cum + a;
-    e.CUM(k) = cum;
+    e.sCUM(k, cum);
     xp = xk; yp = yk; eyp = eyk;
   }
 }
@@ -177,20 +181,22 @@ template <class Env>
 __device__ void arms_invert(Env &e, double prob, WPt &p) {
   int q = e.cnt - 1;
   const double u = prob * e.CUM(q);
-  double cl = e.CUM(q - 1);
+  const double cr0 = e.CUM(q);
+  double cl = e.CUM(q - 1), cr = cr0;
   while (cl > u) {
     q--;
+    cr = cl;
     cl = e.CUM(q - 1);
   }
   p.pr = q;
-  const double cr = e.CUM(q);
   const double prop = (u - cl) / (cr - cl);
   const double xl = e.X(q - 1), xr = e.X(q);
+  const double yr = e.Y(q);
   if (xl == xr) {
-    p.x = xr; p.y = e.Y(q); p.ey = e.EY(q);
+    p.x = xr; p.y = yr; p.ey = expshift(yr, e.ymax);
     return;
   }
-  const double yl = e.Y(q - 1), yr = e.Y(q), eyl = e.EY(q - 1), eyr = e.EY(q);
+  const double yl = e.Y(q - 1), eyl = expshift(yl, e.ymax), eyr = expshift(yr, e.ymax);
   if (fabs(yr - yl) < kYEps) {
     if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
       p.x = xl + ((xr - xl) / (eyr - eyl)) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
@@ -201,7 +207,7 @@ __device__ void arms_invert(Env &e, double prob, WPt &p) {
   } else {
     p.x = xl + ((xr - xl) / (yr - yl)) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
     p.y = ((p.x - xl) / (xr - xl)) * (yr - yl) + yl;
-    p.ey = expshift<Env>(p.y, e.ymax);
+    p.ey = expshift(p.y, e.ymax);
   }
 }
 
@@ -210,25 +216,25 @@ __device__ void arms_update(Env &e, const WPt &p, F &f, Lane &ln) {
   if (e.cnt > kArmsNPoint - 2) return;
   const int pr = p.pr;
   for (int k = e.cnt - 1; k >= pr; k--) {
-    e.X(k + 2) = e.X(k);
-    e.Y(k + 2) = e.Y(k);
+    e.sX(k + 2, e.X(k));
+    e.sY(k + 2, e.Y(k));
   }
   e.cnt += 2;
   const int qi = ((pr - 1) & 1) ? pr + 1 : pr;
-  e.X(qi) = p.x;
-  e.Y(qi) = p.y;
+  e.sX(qi, p.x);
+  e.sY(qi, p.y);
   const int ql = (qi >= 2) ? qi - 2 : qi - 1;
   const int qr = (qi + 2 <= e.cnt - 1) ? qi + 2 : qi + 1;
   const double xl = e.X(ql), xr = e.X(qr);
   if (p.x < (1. - kXEps) * xl + kXEps * xr) {
     const double xn = (1. - kXEps) * xl + kXEps * xr;
-    e.X(qi) = xn;
-    e.Y(qi) = f(xn);
+    e.sX(qi, xn);
+    e.sY(qi, f(xn));
     ln.neval++;
   } else if (p.x > kXEps * xl + (1. - kXEps) * xr) {
     const double xn = kXEps * xl + (1. - kXEps) * xr;
-    e.X(qi) = xn;
-    e.Y(qi) = f(xn);
+    e.sX(qi, xn);
+    e.sY(qi, f(xn));
     ln.neval++;
   }
   arms_meet(e, qi - 1);
@@ -246,14 +252,14 @@ __device__ int arms(Env &e, const double xinit[4], double xl, double xr, F &f, d
   if ((xinit[0] <= xl) || (xinit[3] >= xr)) return 1003;
   if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) return 1004;
   e.cnt = 9;
-  e.X(0) = xl;
+  e.sX(0, xl);
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    e.X(2 * k + 1) = xinit[k];
-    e.Y(2 * k + 1) = f(xinit[k]);
+    e.sX(2 * k + 1, xinit[k]);
+    e.sY(2 * k + 1, f(xinit[k]));
   }
   ln.neval += 4;
-  e.X(8) = xr;
+  e.sX(8, xr);
 #pragma unroll
   for (int k = 0; k < 9; k += 2) arms_meet(e, k);
   arms_cumulate(e);
@@ -273,7 +279,7 @@ __device__ int arms(Env &e, const double xinit[4], double xl, double xr, F &f, d
     ln.neval++;
     if (y >= ynew) {
       p.y = ynew;
-      p.ey = expshift<Env>(p.y, e.ymax);
+      p.ey = expshift(p.y, e.ymax);
       arms_update(e, p, f, ln);
       continue;
     }
@@ -328,77 +334,113 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
   }
 };
 
-template <int NT, class Env, class Sink>
-__device__ void ecs_exact(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
-  const int n = P.n();
-  double target = dev_u(ln.r);
+/* The exact-observation path split into phases so a persistent kernel can
+ * refill lanes between jumps (pht_kernels.hip); ecs_exact() composes them
+ * into the reference's loop (src/Simulate_AbsCTMC_eq_Aslett_ECS.c:231-369). */
+struct EcsLane {
+  double y, t;
+  int j, njump;
+};
+
+template <int NT, class Sink>
+__device__ __forceinline__ void ecs_begin(const Par<NT> &P, double y, Lane &ln, Sink &sk, EcsLane &st) {
+  const double target = dev_u(ln.r);
   const int B = pistart(P, target, ln.flags);
   sk.start(B);
-  double t = 0.0, d;
-  int j = B, lastj;
-  for (int njump = 0;; njump++) {
-    if (njump >= kMaxJumps) {
-      ln.flags |= kFlagJumpCap;
-      break;
-    }
-    const double y_t = y - t;
-    const double Sjj = P.S(j, j);
-    if (P.s(j) > 0.0) {
-      const double U = dev_u(ln.r);
-      double den = 0.0;
+  st.y = y;
+  st.t = 0.0;
+  st.j = B;
+  st.njump = 0;
+}
+
+/* absorb test at the current state (LJMA_probAbsorb + runif, :251-255);
+ * true = the path is complete and its last sojourn has been recorded */
+template <int NT, class Sink>
+__device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink &sk, EcsLane &st) {
+  const int n = P.n();
+  const int j = st.j;
+  bool fin = false;
+  if (st.njump >= kMaxJumps) {
+    ln.flags |= kFlagJumpCap;
+    fin = true;
+  } else if (P.s(j) > 0.0) {
+    const double y_t = st.y - st.t;
+    const double U = dev_u(ln.r);
+    double den = 0.0;
 #pragma unroll
-      for (int i = 0; i < n; i++) den = fma(P.QQs(j, i), pht_exp(P.evals(i) * y_t), den);
-      const double pab = pht_exp(fma(Sjj, y_t, P.logs(j)) - pht_log(den));
-      if (U < pab) break;
-    }
-    lastj = j;
-    EcsDens<NT> f{P, j, y_t, Sjj};
-    double xinit[4];
-    xinit[0] = (y_t) / 1e6;
-    xinit[1] = (y_t) / 3.0;
-    xinit[2] = xinit[1] * 2.0;
-    xinit[3] = y_t - xinit[0];
-    double xsamp = 0.0;
-    const int ainfo = arms(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln);
-    if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
-    t += d = xsamp;
-    /* moveMass over candidates k (P[j,k] != 0) + categorical */
-    const double x = y_t - d;
-    double E[PHT_VEC(NT)];
-#pragma unroll
-    for (int i = 0; i < n; i++) E[i] = pht_exp(P.evals(i) * x);
-    const int cnt = P.nsuccP(j);
-    double w[PHT_VEC(NT)];
-    double sum = 0.0;
-    for (int q = 0; q < cnt; q++) {
-      const int k = P.succP(j, q);
-      double acc = 0.0;
-#pragma unroll
-      for (int i = 0; i < n; i++) acc = fma(P.QQs(k, i), E[i], acc);
-      w[q] = P.P(j, k) * acc;
-      sum += w[q];
-    }
-    target = dev_u(ln.r) * sum;
-    {
-      double sofar = 0.0;
-      int q = 0;
-      for (; q < cnt; q++) {
-        sofar += w[q];
-        if (!(sofar < target)) break;
-      }
-      if (q == cnt) {
-        ln.flags |= kFlagScanEnd;
-        q = cnt - 1;
-      }
-      j = (cnt > 0) ? P.succP(j, q) : 0;
-    }
-    sk.z(lastj, d);
-    sk.N(lastj, j);
-    ln.njump++;
+    for (int i = 0; i < n; i++) den = fma(P.QQs(j, i), pht_exp(P.evals(i) * y_t), den);
+    const double pab = pht_exp(fma(P.S(j, j), y_t, P.logs(j)) - pht_log(den));
+    fin = (U < pab);
   }
-  sk.N(j, j);
-  sk.z(j, y - t);
-  sk.pre(j);
+  if (fin) {
+    sk.N(j, j);
+    sk.z(j, st.y - st.t);
+    sk.pre(j);
+  }
+  return fin;
+}
+
+/* one non-absorbing jump: ARMS sojourn (:307-342), moveMass + categorical
+ * (:350-358), statistics (:362-363) */
+template <int NT, class Env, class Sink>
+__device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane &st) {
+  const int n = P.n();
+  const int j = st.j;
+  const double y_t = st.y - st.t;
+  const double Sjj = P.S(j, j);
+  EcsDens<NT> f{P, j, y_t, Sjj};
+  double xinit[4];
+  xinit[0] = (y_t) / 1e6;
+  xinit[1] = (y_t) / 3.0;
+  xinit[2] = xinit[1] * 2.0;
+  xinit[3] = y_t - xinit[0];
+  double xsamp = 0.0;
+  const int ainfo = arms(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln);
+  if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
+  const double d = xsamp;
+  st.t += d;
+  const double x = y_t - d;
+  double E[PHT_VEC(NT)];
+#pragma unroll
+  for (int i = 0; i < n; i++) E[i] = pht_exp(P.evals(i) * x);
+  const int cnt = P.nsuccP(j);
+  double w[PHT_VEC(NT)];
+  double sum = 0.0;
+  for (int q = 0; q < cnt; q++) {
+    const int k = P.succP(j, q);
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; i++) acc = fma(P.QQs(k, i), E[i], acc);
+    w[q] = P.P(j, k) * acc;
+    sum += w[q];
+  }
+  const double target = dev_u(ln.r) * sum;
+  int nj;
+  {
+    double sofar = 0.0;
+    int q = 0;
+    for (; q < cnt; q++) {
+      sofar += w[q];
+      if (!(sofar < target)) break;
+    }
+    if (q == cnt) {
+      ln.flags |= kFlagScanEnd;
+      q = cnt - 1;
+    }
+    nj = (cnt > 0) ? P.succP(j, q) : 0;
+  }
+  sk.z(j, d);
+  sk.N(j, nj);
+  ln.njump++;
+  st.njump++;
+  st.j = nj;
+}
+
+template <int NT, class Env, class Sink>
+__device__ void ecs_exact(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
+  EcsLane st;
+  ecs_begin(P, y, ln, sk, st);
+  while (!ecs_try_absorb(P, ln, sk, st)) ecs_jump(P, ln, env, sk, st);
 }
 
 /* ===================================================== censored path */

@@ -19,9 +19,10 @@ struct SweepArgs {
   const unsigned char *params; /* packed block (pht_layout.h), device */
   int n;
   int mhit;
+  long begin;                  /* first position of this launch in the shard arrays */
   long count;                  /* observations in this launch */
   const double *y;             /* [count] */
-  const int *cens;             /* [count] */
+  const int *cens;             /* [count]; nullptr = all exact (ECS exact kernel) */
   const uint32_t *gid;         /* [count] global observation index (Philox counter) */
   uint32_t k0, k1, sweep;
   double zscale;               /* 2^zexp */

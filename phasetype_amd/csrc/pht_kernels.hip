@@ -80,8 +80,8 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
   P.iv = reinterpret_cast<const int *>(smem + L.ndouble * 8);
   P.L = L;
 
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < a.count) {
+  const long i = a.begin + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < a.begin + a.count) {
     Lane ln;
     pht_stream_init(&ln.r, a.k0, a.k1, a.gid[i], 0u, a.sweep);
     ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
@@ -94,7 +94,6 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
     }
     const double y = a.y[i];
     Env env;
-    env.bind(threadIdx.x);
     if (METHOD == kMethodMHRS) {
       mhrs<NT>(P, y, a.cens[i], a.mhit, ln, sk);
     } else if (METHOD == kMethodDCS) {
@@ -139,8 +138,136 @@ static int smem_bytes(int n) {
   return L.bytes() + (n + kStatExtra) * 8 + (n + n * n) * 4;
 }
 
+/*
+ * ECS exact observations, persistent lanes.  Block b owns positions
+ * b, b + G, b + 2G, ... of the launch range (G = grid size) and hands them
+ * to its lanes through an LDS cursor: a lane that finishes a path takes the
+ * next observation at once, so the expensive ARMS phase runs with (almost)
+ * all lanes of a wavefront active instead of waiting for the longest path.
+ * The ARMS envelope lives in LDS (EnvLds<kEnvK>), lane-interleaved.
+ */
+constexpr int kEnvK = 11;
+
+template <int NT, bool DEBUG>
+__global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int n = nval<NT>(a.n);
+  const Layout L = make_layout(n);
+  const int pbytes = L.bytes();
+  {
+    const int4 *src = reinterpret_cast<const int4 *>(a.params);
+    int4 *dst = reinterpret_cast<int4 *>(smem);
+    for (int k = threadIdx.x; k < pbytes / 16; k += blockDim.x) dst[k] = src[k];
+  }
+  unsigned long long *zq = reinterpret_cast<unsigned long long *>(smem + pbytes);
+  unsigned long long *xc = zq + n;
+  unsigned *Bc = reinterpret_cast<unsigned *>(xc + kStatExtra);
+  unsigned *Nc = Bc + n;
+  int *cursor = reinterpret_cast<int *>(Nc + n * n);
+  double *envl = reinterpret_cast<double *>(smem + ((pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 15) & ~15));
+  for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
+  for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
+  if (threadIdx.x == 0) *cursor = 0;
+  __syncthreads();
+
+  Par<NT> P;
+  P.d = reinterpret_cast<const double *>(smem);
+  P.iv = reinterpret_cast<const int *>(smem + L.ndouble * 8);
+  P.L = L;
+  EnvLds<kEnvK> env;
+  env.bind(envl, blockDim.x, threadIdx.x);
+  Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
+  Lane ln;
+  EcsLane st;
+  long pos = 0;
+  bool have = false, done = false;
+  for (;;) {
+    bool need = false;
+    while (!done) {
+      if (!have) {
+        const long p = blockIdx.x + (long)atomicAdd(cursor, 1) * gridDim.x;
+        if (p >= a.count) {
+          done = true;
+          break;
+        }
+        pos = a.begin + p;
+        pht_stream_init(&ln.r, a.k0, a.k1, a.gid[pos], 0u, a.sweep);
+        ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
+        if (DEBUG) {
+          sk.dz = a.dbg_zq + pos * n;
+          sk.dN = a.dbg_N + pos * n * n;
+          sk.dB = a.dbg_B + pos;
+          sk.dpre = a.dbg_pre + pos;
+        }
+        ecs_begin(P, a.y[pos], ln, sk, st);
+        have = true;
+      }
+      if (ecs_try_absorb(P, ln, sk, st)) {
+        const uint32_t nd = pht_stream_pos(&ln.r);
+        if (DEBUG) {
+          a.dbg_flags[pos] = ln.flags;
+          a.dbg_ndraw[pos] = nd;
+        }
+        atomicAdd(&xc[0], 1ull);
+        atomicAdd(&xc[1], (unsigned long long)ln.neval);
+        if (ln.flags) atomicAdd(&xc[2], 1ull);
+        atomicAdd(&xc[3], (unsigned long long)nd);
+        atomicAdd(&xc[4], (unsigned long long)ln.njump);
+        have = false;
+        continue;
+      }
+      need = true;
+      break;
+    }
+    if (!__any(need)) break;
+    if (need) ecs_jump(P, ln, env, sk, st);
+  }
+  __syncthreads();
+  unsigned long long *g = a.stats;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    if (zq[k]) atomicAdd(&g[k], zq[k]);
+    if (Bc[k]) atomicAdd(&g[n + k], (unsigned long long)Bc[k]);
+  }
+  for (int k = threadIdx.x; k < n * n; k += blockDim.x)
+    if (Nc[k]) atomicAdd(&g[2 * n + k], (unsigned long long)Nc[k]);
+  for (int k = threadIdx.x; k < kStatExtra; k += blockDim.x)
+    if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
+}
+
+static int smem_bytes_ecs(int n) {
+  return ((smem_bytes(n) + 4 + 15) & ~15) + EnvLds<kEnvK>::lds_doubles_per_lane() * 8 * kBlock;
+}
+
+template <int NT, bool DEBUG>
+static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
+  static int occ = -1, cus = 0;
+  const int sm = smem_bytes_ecs(a.n);
+  if (occ < 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
+    cus = prop.multiProcessorCount;
+    if (hipFuncSetAttribute((const void *)ecs_exact_kernel<NT, DEBUG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            sm) != hipSuccess)
+      return hipErrorUnknown;
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, ecs_exact_kernel<NT, DEBUG>, kBlock, sm) != hipSuccess ||
+        b < 1)
+      b = 1;
+    occ = b;
+  }
+  long want = (a.count + kBlock - 1) / kBlock;
+  long grid = (long)cus * occ;
+  if (grid > want) grid = want;
+  if (grid < 1) return hipSuccess;
+  hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
+  return hipGetLastError();
+}
+
 template <int NT>
 static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStream_t st) {
+  if (method == kMethodECS && a.cens == nullptr) /* exact-only range */
+    return debug ? launch_ecs_exact<NT, true>(a, st) : launch_ecs_exact<NT, false>(a, st);
   const int blocks = (int)((a.count + kBlock - 1) / kBlock);
   if (blocks == 0) return hipSuccess;
   const int sm = smem_bytes(a.n);

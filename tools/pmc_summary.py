@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Summarise tools/prof_pmc.sh output: per-dispatch averages of every counter
+for the sweep kernel, derived ratios, and the corrected HBM traffic
+(MI355X_MICROARCH.md §HBM: FETCH_SIZE counts half the bytes of wide
+coalesced reads on gfx950 — doubled here; WRITE_SIZE as is; both in KiB)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main(d, out=None, kernel_sub="sweep_kernel"):
+    acc = defaultdict(list)
+    bench = None
+    for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
+        per = defaultdict(lambda: defaultdict(float))
+        for row in csv.DictReader(open(f)):
+            if kernel_sub not in row.get("Kernel_Name", ""):
+                continue
+            per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
+        for name, disp in per.items():
+            acc[name].extend(disp.values())
+    for f in sorted(glob.glob(os.path.join(d, "p*.bench.json"))):
+        try:
+            bench = json.load(open(f))
+        except Exception:
+            pass
+    avg = {k: sum(v) / len(v) for k, v in acc.items() if v}
+    res = {"per_dispatch_avg": avg, "dispatches": {k: len(v) for k, v in acc.items()}}
+    der = {}
+    if "SQ_THREAD_CYCLES_VALU" in avg and "SQ_ACTIVE_INST_VALU" in avg:
+        der["valu_lane_utilization"] = avg["SQ_THREAD_CYCLES_VALU"] / (64.0 * avg["SQ_ACTIVE_INST_VALU"])
+    if "FETCH_SIZE" in avg:
+        der["hbm_read_bytes_corrected"] = 2.0 * avg["FETCH_SIZE"] * 1024
+    if "WRITE_SIZE" in avg:
+        der["hbm_write_bytes"] = avg["WRITE_SIZE"] * 1024
+    if "hbm_read_bytes_corrected" in der and "hbm_write_bytes" in der:
+        der["hbm_bytes_per_launch"] = der["hbm_read_bytes_corrected"] + der["hbm_write_bytes"]
+    if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
+        der["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(1.0, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+    if bench:
+        kms = bench["roofline"]["kernel_ms"]
+        der["kernel_ms_unprofiled_bench"] = kms
+        if "SQ_INSTS_VALU_FLOPS_FP64" in avg:
+            der["fp64_tflops_at_bench_time"] = avg["SQ_INSTS_VALU_FLOPS_FP64"] / (kms * 1e-3) / 1e12
+    res["derived"] = der
+    js = json.dumps(res, indent=1, sort_keys=True)
+    print(js)
+    if out:
+        open(out, "w").write(js)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
