@@ -30,6 +30,10 @@
 #include "pht_layout.h"
 #include "pht_philox.h"
 
+/* LDS (address space 3) qualifier: pointers into the workgroup's LDS must
+ * carry it, or hipcc emits generic FLAT loads/stores instead of ds_* */
+#define PHT_LDS __attribute__((address_space(3)))
+
 namespace pht {
 
 /* flag bits (per observation) */
@@ -49,32 +53,41 @@ constexpr double kXEps = 0.00001, kYEps = 0.1, kEYEps = 0.001, kYCeil = 50.;
 /* parameter block accessor (pointers into LDS or global memory) */
 template <int NT>
 struct Par {
-  const double *d;
-  const int *iv;
-  Layout L;
-  __device__ __forceinline__ int n() const { return NT > 0 ? NT : L.n; }
-  __device__ __forceinline__ double evals(int i) const { return d[L.evals + i]; }
-  __device__ __forceinline__ double s(int i) const { return d[L.s + i]; }
-  __device__ __forceinline__ double logs(int i) const { return d[L.logs + i]; }
-  __device__ __forceinline__ double scale(int i) const { return d[L.scale + i]; }
-  __device__ __forceinline__ double logscale(int i) const { return d[L.logscale + i]; }
-  __device__ __forceinline__ double piQ(int i) const { return d[L.piQ + i]; }
-  __device__ __forceinline__ double pi(int i) const { return d[L.pi + i]; }
-  __device__ __forceinline__ double S(int i, int j) const { return d[L.S + i + j * n()]; }
-  __device__ __forceinline__ double P(int i, int j) const { return d[L.P + i + j * n()]; }
-  __device__ __forceinline__ double Pf(int i, int j) const { return d[L.Pf + i + j * n()]; }
-  __device__ __forceinline__ double QQs(int i, int j) const { return d[L.QQs + i + j * n()]; }
-  __device__ __forceinline__ double W(int i, int j) const { return d[L.W + i + j * n()]; }
-  __device__ __forceinline__ double QQ1(int i, int j) const { return d[L.QQ1 + i + j * n()]; }
-  __device__ __forceinline__ double V(int i, int j) const { return d[L.V + i + j * n()]; }
-  __device__ __forceinline__ double Q(int i, int j) const { return d[L.Q + i + j * n()]; }
-  __device__ __forceinline__ double Qinv(int i, int j) const { return d[L.Qinv + i + j * n()]; }
-  __device__ __forceinline__ int nsuccP(int j) const { return iv[L.nsuccP + j]; }
-  __device__ __forceinline__ int succP(int j, int q) const { return iv[L.succP + j * n() + q]; }
-  __device__ __forceinline__ int nsuccPf(int j) const { return iv[L.nsuccPf + j]; }
-  __device__ __forceinline__ int succPf(int j, int q) const { return iv[L.succPf + j * (n() + 1) + q]; }
-  __device__ __forceinline__ int nsuccS(int j) const { return iv[L.nsuccS + j]; }
-  __device__ __forceinline__ int succS(int j, int q) const { return iv[L.succS + j * n() + q]; }
+  const PHT_LDS double *d;
+  const PHT_LDS int *iv;
+  Layout Lr; /* runtime layout (NT == 0) */
+  /* offsets: compile-time constants when NT > 0 */
+  __device__ __forceinline__ Layout lay() const {
+    if constexpr (NT > 0) {
+      constexpr Layout c = make_layout(NT);
+      return c;
+    } else {
+      return Lr;
+    }
+  }
+  __device__ __forceinline__ int n() const { return NT > 0 ? NT : Lr.n; }
+  __device__ __forceinline__ double evals(int i) const { return d[lay().evals + i]; }
+  __device__ __forceinline__ double s(int i) const { return d[lay().s + i]; }
+  __device__ __forceinline__ double logs(int i) const { return d[lay().logs + i]; }
+  __device__ __forceinline__ double scale(int i) const { return d[lay().scale + i]; }
+  __device__ __forceinline__ double logscale(int i) const { return d[lay().logscale + i]; }
+  __device__ __forceinline__ double piQ(int i) const { return d[lay().piQ + i]; }
+  __device__ __forceinline__ double pi(int i) const { return d[lay().pi + i]; }
+  __device__ __forceinline__ double S(int i, int j) const { return d[lay().S + i + j * n()]; }
+  __device__ __forceinline__ double P(int i, int j) const { return d[lay().P + i + j * n()]; }
+  __device__ __forceinline__ double Pf(int i, int j) const { return d[lay().Pf + i + j * n()]; }
+  __device__ __forceinline__ double QQs(int i, int j) const { return d[lay().QQs + i + j * n()]; }
+  __device__ __forceinline__ double W(int i, int j) const { return d[lay().W + i + j * n()]; }
+  __device__ __forceinline__ double QQ1(int i, int j) const { return d[lay().QQ1 + i + j * n()]; }
+  __device__ __forceinline__ double V(int i, int j) const { return d[lay().V + i + j * n()]; }
+  __device__ __forceinline__ double Q(int i, int j) const { return d[lay().Q + i + j * n()]; }
+  __device__ __forceinline__ double Qinv(int i, int j) const { return d[lay().Qinv + i + j * n()]; }
+  __device__ __forceinline__ int nsuccP(int j) const { return iv[lay().nsuccP + j]; }
+  __device__ __forceinline__ int succP(int j, int q) const { return iv[lay().succP + j * n() + q]; }
+  __device__ __forceinline__ int nsuccPf(int j) const { return iv[lay().nsuccPf + j]; }
+  __device__ __forceinline__ int succPf(int j, int q) const { return iv[lay().succPf + j * (n() + 1) + q]; }
+  __device__ __forceinline__ int nsuccS(int j) const { return iv[lay().nsuccS + j]; }
+  __device__ __forceinline__ int succS(int j, int q) const { return iv[lay().succS + j * n() + q]; }
 };
 
 #define PHT_VEC(NT) ((NT) > 0 ? (NT) : kMaxN)
@@ -111,7 +124,7 @@ __device__ __forceinline__ double expshift(double y, double y0) {
 __device__ __forceinline__ double logshift(double y, double y0) { return pht_log(y) + y0 - kYCeil; }
 
 template <class Env>
-__device__ void arms_meet(Env &e, int k) {
+__device__ __forceinline__ void arms_meet(Env &e, int k) {
   double gl = 0.0, gr = 0.0, grl = 0.0, dl = 0.0, dr = 0.0;
   const int last = e.cnt - 1;
   const bool il = (k >= 3), ir = (k + 3 <= last), irl = (k >= 1 && k + 1 <= last);
@@ -148,7 +161,7 @@ __device__ void arms_meet(Env &e, int k) {
 }
 
 template <class Env>
-__device__ void arms_cumulate(Env &e) {
+__device__ __forceinline__ void arms_cumulate(Env &e) {
   double ymax = e.Y(0);
   for (int k = 1; k < e.cnt; k++) {
     const double yk = e.Y(k);
@@ -178,7 +191,7 @@ struct WPt {
 };
 
 template <class Env>
-__device__ void arms_invert(Env &e, double prob, WPt &p) {
+__device__ __forceinline__ void arms_invert(Env &e, double prob, WPt &p) {
   int q = e.cnt - 1;
   const double u = prob * e.CUM(q);
   const double cr0 = e.CUM(q);
@@ -212,7 +225,7 @@ __device__ void arms_invert(Env &e, double prob, WPt &p) {
 }
 
 template <class Env, class F>
-__device__ void arms_update(Env &e, const WPt &p, F &f, Lane &ln) {
+__device__ __forceinline__ void arms_update(Env &e, const WPt &p, F &f, Lane &ln) {
   if (e.cnt > kArmsNPoint - 2) return;
   const int pr = p.pr;
   for (int k = e.cnt - 1; k >= pr; k--) {
@@ -247,7 +260,7 @@ __device__ void arms_update(Env &e, const WPt &p, F &f, Lane &ln) {
 /* arms() as used by the reference (xprev 0, one sample).  Returns 0, an
  * initial-point error code, or 4 on the iteration cap. */
 template <class Env, class F>
-__device__ int arms(Env &e, const double xinit[4], double xl, double xr, F &f, double xprev, double &xsamp,
+__device__ __forceinline__ int arms(Env &e, const double xinit[4], double xl, double xr, F &f, double xprev, double &xsamp,
                     Lane &ln) {
   if ((xinit[0] <= xl) || (xinit[3] >= xr)) return 1003;
   if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) return 1004;
@@ -437,7 +450,7 @@ __device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, S
 }
 
 template <int NT, class Env, class Sink>
-__device__ void ecs_exact(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
+__device__ __forceinline__ void ecs_exact(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
   EcsLane st;
   ecs_begin(P, y, ln, sk, st);
   while (!ecs_try_absorb(P, ln, sk, st)) ecs_jump(P, ln, env, sk, st);
@@ -466,7 +479,7 @@ struct CjDens { /* log F_{P_j}(y - t - d) + log dexp(d; 1/-S_jj) */
 };
 
 template <int NT, class Env, class Sink>
-__device__ void censored(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
+__device__ __forceinline__ void censored(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
   const int n = P.n();
   double target = dev_u(ln.r);
   const int B = pistart(P, target, ln.flags);
@@ -567,7 +580,7 @@ __device__ void censored(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &s
 /* One LJMA_samplechain_Bladt call: returns pre; pos = stream position of
  * the accepted attempt (replayed later for the statistics). */
 template <int NT>
-__device__ int bladt_chain(const Par<NT> &P, double y, int cens, Lane &ln, uint32_t &pos) {
+__device__ __forceinline__ int bladt_chain(const Par<NT> &P, double y, int cens, Lane &ln, uint32_t &pos) {
   const int n = P.n();
   double t = 0.0;
   int lastj = 0, natt = 0;
@@ -612,7 +625,7 @@ __device__ int bladt_chain(const Par<NT> &P, double y, int cens, Lane &ln, uint3
 }
 
 template <int NT, class Sink>
-__device__ void bladt_replay(const Par<NT> &P, double y, int cens, Lane &ln, uint32_t pos, Sink &sk) {
+__device__ __forceinline__ void bladt_replay(const Par<NT> &P, double y, int cens, Lane &ln, uint32_t pos, Sink &sk) {
   const int n = P.n();
   pht_stream r = ln.r;
   pht_stream_seek(&r, pos);
@@ -661,7 +674,7 @@ __device__ void bladt_replay(const Par<NT> &P, double y, int cens, Lane &ln, uin
 }
 
 template <int NT, class Sink>
-__device__ void mhrs(const Par<NT> &P, double y, int cens, int mhit, Lane &ln, Sink &sk) {
+__device__ __forceinline__ void mhrs(const Par<NT> &P, double y, int cens, int mhit, Lane &ln, Sink &sk) {
   uint32_t cpos = 0, ppos = 0;
   int cpre = bladt_chain(P, y, cens, ln, cpos);
   while (P.s(cpre) == 0) cpre = bladt_chain(P, y, cens, ln, cpos);
@@ -703,7 +716,7 @@ struct HobCdf {
 };
 
 template <class F>
-__device__ double find02(double ax, double bx, double fa, double fb, const F &f, double *Tol, int *Maxit,
+__device__ __forceinline__ double find02(double ax, double bx, double fa, double fb, const F &f, double *Tol, int *Maxit,
                          int &nevals) {
   double a, b, c, fc, tol;
   int maxit;
@@ -753,7 +766,7 @@ __device__ double find02(double ax, double bx, double fa, double fb, const F &f,
 }
 
 template <int NT, class Sink>
-__device__ void dcs(const Par<NT> &P, double y, Lane &ln, Sink &sk) {
+__device__ __forceinline__ void dcs(const Par<NT> &P, double y, Lane &ln, Sink &sk) {
   const int n = P.n();
   /* end state b ~ (pi e^{yS})_b s_b */
   double a[PHT_VEC(NT)];

@@ -20,6 +20,10 @@
 
 #include <hip/hip_runtime.h>
 
+#ifndef PHT_LDS
+#define PHT_LDS __attribute__((address_space(3)))
+#endif
+
 namespace pht {
 
 struct EnvPrivate {
@@ -34,26 +38,38 @@ struct EnvPrivate {
   __device__ __forceinline__ void sCUM(int k, double v) { cum[k] = v; }
 };
 
-template <int K>
+#ifndef PHT_PRIV
+#define PHT_PRIV __attribute__((address_space(5)))
+#endif
+
+/* K points per lane in LDS (stride = threads per block), the rest in a
+ * separate private spill array (kept out of this struct so that cnt, ymax
+ * and the LDS base stay in registers). */
+template <int K, int STRIDE>
 struct EnvLds {
-  double *lx, *ly, *lc; /* LDS: lane's element 0; element k at +k*stride */
-  int stride;
-  double ox[100 - K], oy[100 - K], oc[100 - K];
+  static constexpr int kSpill = 100 - K;
+  PHT_LDS double *l;  /* lane's element 0 */
+  PHT_PRIV double *ov; /* [3][kSpill] */
   int cnt;
   double ymax;
-  __device__ __forceinline__ void bind(double *lds, int nthreads, int tid) {
-    stride = nthreads;
-    lx = lds + tid;
-    ly = lds + K * nthreads + tid;
-    lc = lds + 2 * K * nthreads + tid;
+  __device__ __forceinline__ void bind(PHT_LDS double *lds, int tid, PHT_PRIV double *spill) {
+    l = lds + tid;
+    ov = spill;
   }
   static constexpr int lds_doubles_per_lane() { return 3 * K; }
-  __device__ __forceinline__ double X(int k) const { if (k < K) return lx[k * stride]; return ox[k - K]; }
-  __device__ __forceinline__ double Y(int k) const { if (k < K) return ly[k * stride]; return oy[k - K]; }
-  __device__ __forceinline__ double CUM(int k) const { if (k < K) return lc[k * stride]; return oc[k - K]; }
-  __device__ __forceinline__ void sX(int k, double v) { if (k < K) lx[k * stride] = v; else ox[k - K] = v; }
-  __device__ __forceinline__ void sY(int k, double v) { if (k < K) ly[k * stride] = v; else oy[k - K] = v; }
-  __device__ __forceinline__ void sCUM(int k, double v) { if (k < K) lc[k * stride] = v; else oc[k - K] = v; }
+  __device__ __forceinline__ double X(int k) const { if (k < K) return l[k * STRIDE]; return ov[k - K]; }
+  __device__ __forceinline__ double Y(int k) const { if (k < K) return l[(K + k) * STRIDE]; return ov[kSpill + k - K]; }
+  __device__ __forceinline__ double CUM(int k) const {
+    if (k < K) return l[(2 * K + k) * STRIDE];
+    return ov[2 * kSpill + k - K];
+  }
+  __device__ __forceinline__ void sX(int k, double v) { if (k < K) l[k * STRIDE] = v; else ov[k - K] = v; }
+  __device__ __forceinline__ void sY(int k, double v) {
+    if (k < K) l[(K + k) * STRIDE] = v; else ov[kSpill + k - K] = v;
+  }
+  __device__ __forceinline__ void sCUM(int k, double v) {
+    if (k < K) l[(2 * K + k) * STRIDE] = v; else ov[2 * kSpill + k - K] = v;
+  }
 };
 
 }  // namespace pht

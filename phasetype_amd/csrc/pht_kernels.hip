@@ -24,11 +24,16 @@ namespace pht {
 
 /* Statistics sink: workgroup accumulators in LDS (+ per-observation debug
  * rows in global memory when DEBUG). */
+template <class T>
+__device__ __forceinline__ void lds_add(PHT_LDS T *p, T v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <bool DEBUG>
 struct Sink {
-  unsigned long long *zq; /* LDS [n] */
-  unsigned *Bc;           /* LDS [n] */
-  unsigned *Nc;           /* LDS [n*n] */
+  PHT_LDS unsigned long long *zq; /* LDS [n] */
+  PHT_LDS unsigned *Bc;           /* LDS [n] */
+  PHT_LDS unsigned *Nc;           /* LDS [n*n] */
   int n;
   double zscale;
   long long *dz;          /* debug row [n] */
@@ -36,15 +41,15 @@ struct Sink {
   int *dB, *dpre;
   __device__ __forceinline__ void z(int k, double d) {
     const long long q = (long long)rint(d * zscale);
-    atomicAdd(&zq[k], (unsigned long long)q);
+    lds_add(&zq[k], (unsigned long long)q);
     if (DEBUG) dz[k] += q;
   }
   __device__ __forceinline__ void N(int i, int j) {
-    atomicAdd(&Nc[i + j * n], 1u);
+    lds_add(&Nc[i + j * n], 1u);
     if (DEBUG) dN[i + j * n] += 1;
   }
   __device__ __forceinline__ void start(int b) {
-    atomicAdd(&Bc[b], 1u);
+    lds_add(&Bc[b], 1u);
     if (DEBUG) *dB = b;
   }
   __device__ __forceinline__ void pre(int j) {
@@ -63,22 +68,23 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
   const int pbytes = L.bytes();
   /* stage the parameter block */
   {
-    const int4 *src = reinterpret_cast<const int4 *>(a.params);
-    int4 *dst = reinterpret_cast<int4 *>(smem);
-    for (int k = threadIdx.x; k < pbytes / 16; k += blockDim.x) dst[k] = src[k];
+    const unsigned long long *src = reinterpret_cast<const unsigned long long *>(a.params);
+    PHT_LDS unsigned long long *dst = (PHT_LDS unsigned long long *)smem;
+    for (int k = threadIdx.x; k < pbytes / 8; k += blockDim.x) dst[k] = src[k];
   }
-  unsigned long long *zq = reinterpret_cast<unsigned long long *>(smem + pbytes);
-  unsigned long long *xc = zq + n; /* kStatExtra counters */
-  unsigned *Bc = reinterpret_cast<unsigned *>(xc + kStatExtra);
-  unsigned *Nc = Bc + n;
+  PHT_LDS unsigned char *lsm = (PHT_LDS unsigned char *)smem;
+  PHT_LDS unsigned long long *zq = (PHT_LDS unsigned long long *)(lsm + pbytes);
+  PHT_LDS unsigned long long *xc = zq + n; /* kStatExtra counters */
+  PHT_LDS unsigned *Bc = (PHT_LDS unsigned *)(xc + kStatExtra);
+  PHT_LDS unsigned *Nc = Bc + n;
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
   __syncthreads();
 
   Par<NT> P;
-  P.d = reinterpret_cast<const double *>(smem);
-  P.iv = reinterpret_cast<const int *>(smem + L.ndouble * 8);
-  P.L = L;
+  P.d = (const PHT_LDS double *)lsm;
+  P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
+  P.Lr = L;
 
   const long i = a.begin + (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < a.begin + a.count) {
@@ -107,12 +113,12 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
       a.dbg_flags[i] = ln.flags;
       a.dbg_ndraw[i] = nd;
     }
-    atomicAdd(&xc[0], 1ull);
-    atomicAdd(&xc[1], (unsigned long long)ln.neval);
-    if (ln.flags) atomicAdd(&xc[2], 1ull);
-    atomicAdd(&xc[3], (unsigned long long)nd);
-    atomicAdd(&xc[4], (unsigned long long)ln.njump);
-    atomicAdd(&xc[5], (unsigned long long)ln.nbrent);
+    lds_add(&xc[0], 1ull);
+    lds_add(&xc[1], (unsigned long long)ln.neval);
+    if (ln.flags) lds_add(&xc[2], 1ull);
+    lds_add(&xc[3], (unsigned long long)nd);
+    lds_add(&xc[4], (unsigned long long)ln.njump);
+    lds_add(&xc[5], (unsigned long long)ln.nbrent);
   }
   __syncthreads();
   /* flush: [zq n][B n][N n*n][extra] */
@@ -155,27 +161,29 @@ __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
   const Layout L = make_layout(n);
   const int pbytes = L.bytes();
   {
-    const int4 *src = reinterpret_cast<const int4 *>(a.params);
-    int4 *dst = reinterpret_cast<int4 *>(smem);
-    for (int k = threadIdx.x; k < pbytes / 16; k += blockDim.x) dst[k] = src[k];
+    const unsigned long long *src = reinterpret_cast<const unsigned long long *>(a.params);
+    PHT_LDS unsigned long long *dst = (PHT_LDS unsigned long long *)smem;
+    for (int k = threadIdx.x; k < pbytes / 8; k += blockDim.x) dst[k] = src[k];
   }
-  unsigned long long *zq = reinterpret_cast<unsigned long long *>(smem + pbytes);
-  unsigned long long *xc = zq + n;
-  unsigned *Bc = reinterpret_cast<unsigned *>(xc + kStatExtra);
-  unsigned *Nc = Bc + n;
-  int *cursor = reinterpret_cast<int *>(Nc + n * n);
-  double *envl = reinterpret_cast<double *>(smem + ((pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 15) & ~15));
+  PHT_LDS unsigned char *lsm = (PHT_LDS unsigned char *)smem;
+  PHT_LDS unsigned long long *zq = (PHT_LDS unsigned long long *)(lsm + pbytes);
+  PHT_LDS unsigned long long *xc = zq + n;
+  PHT_LDS unsigned *Bc = (PHT_LDS unsigned *)(xc + kStatExtra);
+  PHT_LDS unsigned *Nc = Bc + n;
+  PHT_LDS int *cursor = (PHT_LDS int *)(Nc + n * n);
+  PHT_LDS double *envl = (PHT_LDS double *)(lsm + ((pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 15) & ~15));
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
   if (threadIdx.x == 0) *cursor = 0;
   __syncthreads();
 
   Par<NT> P;
-  P.d = reinterpret_cast<const double *>(smem);
-  P.iv = reinterpret_cast<const int *>(smem + L.ndouble * 8);
-  P.L = L;
-  EnvLds<kEnvK> env;
-  env.bind(envl, blockDim.x, threadIdx.x);
+  P.d = (const PHT_LDS double *)lsm;
+  P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
+  P.Lr = L;
+  EnvLds<kEnvK, kBlock> env;
+  double spill[3 * EnvLds<kEnvK, kBlock>::kSpill];
+  env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill);
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
   Lane ln;
   EcsLane st;
@@ -185,7 +193,7 @@ __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
     bool need = false;
     while (!done) {
       if (!have) {
-        const long p = blockIdx.x + (long)atomicAdd(cursor, 1) * gridDim.x;
+        const long p = blockIdx.x + (long)__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) * gridDim.x;
         if (p >= a.count) {
           done = true;
           break;
@@ -208,11 +216,11 @@ __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
           a.dbg_flags[pos] = ln.flags;
           a.dbg_ndraw[pos] = nd;
         }
-        atomicAdd(&xc[0], 1ull);
-        atomicAdd(&xc[1], (unsigned long long)ln.neval);
-        if (ln.flags) atomicAdd(&xc[2], 1ull);
-        atomicAdd(&xc[3], (unsigned long long)nd);
-        atomicAdd(&xc[4], (unsigned long long)ln.njump);
+        lds_add(&xc[0], 1ull);
+        lds_add(&xc[1], (unsigned long long)ln.neval);
+        if (ln.flags) lds_add(&xc[2], 1ull);
+        lds_add(&xc[3], (unsigned long long)nd);
+        lds_add(&xc[4], (unsigned long long)ln.njump);
         have = false;
         continue;
       }
@@ -235,7 +243,7 @@ __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
 }
 
 static int smem_bytes_ecs(int n) {
-  return ((smem_bytes(n) + 4 + 15) & ~15) + EnvLds<kEnvK>::lds_doubles_per_lane() * 8 * kBlock;
+  return ((smem_bytes(n) + 4 + 15) & ~15) + EnvLds<kEnvK, kBlock>::lds_doubles_per_lane() * 8 * kBlock;
 }
 
 template <int NT, bool DEBUG>

@@ -26,9 +26,9 @@
 #define PHT_LAYOUT_H
 
 #if defined(__HIPCC__)
-#define PHT_LHD __host__ __device__ __forceinline__
+#define PHT_LHD __host__ __device__ constexpr
 #else
-#define PHT_LHD inline
+#define PHT_LHD constexpr
 #endif
 
 namespace pht {
@@ -45,7 +45,7 @@ struct Layout {
 };
 
 PHT_LHD Layout make_layout(int n) {
-  Layout L;
+  Layout L{};
   int o = 0, nn = n * n;
   L.n = n;
   L.evals = o; o += n;

@@ -11,7 +11,7 @@ import sys
 from collections import defaultdict
 
 
-def main(d, out=None, kernel_sub="sweep_kernel"):
+def main(d, out=None, kernel_sub="pht::"):
     acc = defaultdict(list)
     bench = None
     for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
