@@ -337,12 +337,31 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
   const Par<NT> &P;
   int j;
   double y_t, Sjj;
-  __device__ __forceinline__ double operator()(double d) const {
+  /* exponentials of the absorb test at this state, e^{λ_i y_t} (= the
+   * density's at d = 0), and of the most recent evaluation: reused, not
+   * recomputed (same expression, same operands: bit-identical) */
+  const double *E0;
+  bool haveE0;
+  double lastd;
+  double Elast[PHT_VEC(NT)];
+  __device__ __forceinline__ double operator()(double d) {
     const int n = P.n();
     const double x = y_t - d;
     double acc = 0.0;
+    if (haveE0 && d == 0.0) {
 #pragma unroll
-    for (int i = 0; i < n; i++) acc = fma(P.W(j, i), pht_exp(P.evals(i) * x), acc);
+      for (int i = 0; i < n; i++) {
+        Elast[i] = E0[i];
+        acc = fma(P.W(j, i), E0[i], acc);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < n; i++) {
+        Elast[i] = pht_exp(P.evals(i) * x);
+        acc = fma(P.W(j, i), Elast[i], acc);
+      }
+    }
+    lastd = d;
     return pht_log(acc) + Sjj * d;
   }
 };
@@ -350,13 +369,16 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
 /* The exact-observation path split into phases so a persistent kernel can
  * refill lanes between jumps (pht_kernels.hip); ecs_exact() composes them
  * into the reference's loop (src/Simulate_AbsCTMC_eq_Aslett_ECS.c:231-369). */
+template <int NT>
 struct EcsLane {
   double y, t;
   int j, njump;
+  bool haveE0;               /* E0 valid for the current state and time */
+  double E0[PHT_VEC(NT)];    /* e^{λ_i (y - t)} from the absorb test */
 };
 
 template <int NT, class Sink>
-__device__ __forceinline__ void ecs_begin(const Par<NT> &P, double y, Lane &ln, Sink &sk, EcsLane &st) {
+__device__ __forceinline__ void ecs_begin(const Par<NT> &P, double y, Lane &ln, Sink &sk, EcsLane<NT> &st) {
   const double target = dev_u(ln.r);
   const int B = pistart(P, target, ln.flags);
   sk.start(B);
@@ -369,10 +391,11 @@ __device__ __forceinline__ void ecs_begin(const Par<NT> &P, double y, Lane &ln, 
 /* absorb test at the current state (LJMA_probAbsorb + runif, :251-255);
  * true = the path is complete and its last sojourn has been recorded */
 template <int NT, class Sink>
-__device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink &sk, EcsLane &st) {
+__device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink &sk, EcsLane<NT> &st) {
   const int n = P.n();
   const int j = st.j;
   bool fin = false;
+  st.haveE0 = false;
   if (st.njump >= kMaxJumps) {
     ln.flags |= kFlagJumpCap;
     fin = true;
@@ -381,7 +404,11 @@ __device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink 
     const double U = dev_u(ln.r);
     double den = 0.0;
 #pragma unroll
-    for (int i = 0; i < n; i++) den = fma(P.QQs(j, i), pht_exp(P.evals(i) * y_t), den);
+    for (int i = 0; i < n; i++) {
+      st.E0[i] = pht_exp(P.evals(i) * y_t);
+      den = fma(P.QQs(j, i), st.E0[i], den);
+    }
+    st.haveE0 = true;
     const double pab = pht_exp(fma(P.S(j, j), y_t, P.logs(j)) - pht_log(den));
     fin = (U < pab);
   }
@@ -396,12 +423,12 @@ __device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink 
 /* one non-absorbing jump: ARMS sojourn (:307-342), moveMass + categorical
  * (:350-358), statistics (:362-363) */
 template <int NT, class Env, class Sink>
-__device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane &st) {
+__device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st) {
   const int n = P.n();
   const int j = st.j;
   const double y_t = st.y - st.t;
   const double Sjj = P.S(j, j);
-  EcsDens<NT> f{P, j, y_t, Sjj};
+  EcsDens<NT> f{P, j, y_t, Sjj, st.E0, st.haveE0, -1.0, {}};
   double xinit[4];
   xinit[0] = (y_t) / 1e6;
   xinit[1] = (y_t) / 3.0;
@@ -413,34 +440,50 @@ __device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, S
   const double d = xsamp;
   st.t += d;
   const double x = y_t - d;
+  /* e^{λ_i (y_t - d)}: the accepted proposal's density evaluation already
+   * computed them (d = lastd), or d = 0 = the absorb test's */
   double E[PHT_VEC(NT)];
+  if (d == f.lastd) {
 #pragma unroll
-  for (int i = 0; i < n; i++) E[i] = pht_exp(P.evals(i) * x);
+    for (int i = 0; i < n; i++) E[i] = f.Elast[i];
+  } else if (d == 0.0 && st.haveE0) {
+#pragma unroll
+    for (int i = 0; i < n; i++) E[i] = st.E0[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < n; i++) E[i] = pht_exp(P.evals(i) * x);
+  }
   const int cnt = P.nsuccP(j);
   double w[PHT_VEC(NT)];
   double sum = 0.0;
-  for (int q = 0; q < cnt; q++) {
-    const int k = P.succP(j, q);
-    double acc = 0.0;
 #pragma unroll
-    for (int i = 0; i < n; i++) acc = fma(P.QQs(k, i), E[i], acc);
-    w[q] = P.P(j, k) * acc;
-    sum += w[q];
+  for (int q = 0; q < PHT_VEC(NT); q++) {
+    if (q < cnt) {
+      const int k = P.succP(j, q);
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) acc = fma(P.QQs(k, i), E[i], acc);
+      w[q] = P.P(j, k) * acc;
+      sum += w[q];
+    }
   }
   const double target = dev_u(ln.r) * sum;
   int nj;
   {
     double sofar = 0.0;
-    int q = 0;
-    for (; q < cnt; q++) {
-      sofar += w[q];
-      if (!(sofar < target)) break;
+    int sel = -1;
+#pragma unroll
+    for (int q = 0; q < PHT_VEC(NT); q++) {
+      if (q < cnt && sel < 0) {
+        sofar += w[q];
+        if (!(sofar < target)) sel = q;
+      }
     }
-    if (q == cnt) {
+    if (sel < 0) {
       ln.flags |= kFlagScanEnd;
-      q = cnt - 1;
+      sel = cnt - 1;
     }
-    nj = (cnt > 0) ? P.succP(j, q) : 0;
+    nj = (cnt > 0) ? P.succP(j, sel) : 0;
   }
   sk.z(j, d);
   sk.N(j, nj);
@@ -451,7 +494,7 @@ __device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, S
 
 template <int NT, class Env, class Sink>
 __device__ __forceinline__ void ecs_exact(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
-  EcsLane st;
+  EcsLane<NT> st;
   ecs_begin(P, y, ln, sk, st);
   while (!ecs_try_absorb(P, ln, sk, st)) ecs_jump(P, ln, env, sk, st);
 }

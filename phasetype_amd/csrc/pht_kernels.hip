@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
   env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill);
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
   Lane ln;
-  EcsLane st;
+  EcsLane<NT> st;
   long pos = 0;
   bool have = false, done = false;
   for (;;) {
