@@ -110,31 +110,44 @@ static const double pht_exp_tab[128] = {
     0x1.fa7c1819e90d8p+0, 0x1.74853f3a5931ep-55,
 };
 
+/* Where the device reads the tables: by default the __constant__ copies
+ * (vector-memory loads through the L1); with PHT_DETMATH_LDS, workgroup LDS
+ * copies that every kernel stages first (pht_stage_math_tables). */
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PHT_DETMATH_LDS)
+__shared__ double pht_lds_exp_tab[128];
+__shared__ double pht_lds_log_tab[768];
+#define PHT_EXP_TAB pht_lds_exp_tab
+#define PHT_LOG_TAB pht_lds_log_tab
+#else
+#define PHT_EXP_TAB pht_exp_tab
+#define PHT_LOG_TAB pht_log_tab
+#endif
+
 PHT_HD double pht_exp(double x) {
+  /* straight-line (no branches: on the GPU every special case is a select) */
   const double INV_LN2_N = 0x1.71547652b82fep+6; /* 64/ln2 */
   const double LN2_HI_N = 0x1.62e42fefa39efp-7;  /* ln2/64 rounded */
   const double LN2_LO_N = 0x1.abc9e3b39803fp-62; /* ln2/64 - LN2_HI_N */
   const double SHIFT = 6755399441055744.0;       /* 1.5 * 2^52 */
-  if (x != x) return x;
-  if (x > 709.782712893383973096) return INFINITY;
-  if (x < -745.133219101941108420) return 0.0;
-  const double kd = fma(x, INV_LN2_N, SHIFT) - SHIFT; /* round-to-nearest-even integer */
-  double r = fma(-kd, LN2_HI_N, x);
+  const double HI = 709.782712893383973096, LO = -745.133219101941108420;
+  const double xc = (x > HI) ? HI : ((x < LO) ? LO : x); /* NaN passes through */
+  const double kd = fma(xc, INV_LN2_N, SHIFT) - SHIFT;   /* round-to-nearest-even integer */
+  double r = fma(-kd, LN2_HI_N, xc);
   r = fma(-kd, LN2_LO_N, r); /* |r| <= ln2/128 */
-  const int ki = (int)kd;
+  const int ki = (xc == xc) ? (int)kd : 0;
   const int idx = ki & 63;
   const int k = ki >> 6; /* floor(ki / 64) */
-  const double sc = pht_exp_tab[2 * idx], tail = pht_exp_tab[2 * idx + 1];
+  const double sc = PHT_EXP_TAB[2 * idx], tail = PHT_EXP_TAB[2 * idx + 1];
   double q = 1.3888888888888889419e-03;   /* 1/6! */
   q = fma(q, r, 8.3333333333333332177e-03); /* 1/5! */
   q = fma(q, r, 4.1666666666666664354e-02); /* 1/4! */
   q = fma(q, r, 1.6666666666666665741e-01); /* 1/3! */
   q = fma(q, r, 0.5);
   const double p = fma(r * r, q, r); /* e^r - 1 */
-  const double res = sc + fma(sc, p, tail);
-  if (k > 1023) return res * 2.0 * pht_u2d((uint64_t)(k - 1 + 1023) << 52);
-  if (k < -1022) return (res * pht_u2d((uint64_t)(k + 54 + 1023) << 52)) * 5.5511151231257827021e-17; /* 2^-54 */
-  return res * pht_u2d((uint64_t)(k + 1023) << 52);
+  /* res * 2^k with one rounding (subnormal results) */
+  const double res = ldexp(sc + fma(sc, p, tail), k);
+  const double out = (x > HI) ? INFINITY : ((x < LO) ? 0.0 : res);
+  return (x != x) ? x : out;
 }
 
 /* log table, index i + 128 h (i = top 7 mantissa bits of m in [1,2), h = 1
@@ -405,32 +418,20 @@ static const double pht_log_tab[768] = {
 };
 
 PHT_HD double pht_log(double x) {
+  /* straight-line (no branches: on the GPU every special case is a select) */
   const double LN2_HI = 0x1.62e42fee00000p-1; /* 21 trailing zero bits: k*LN2_HI exact */
   const double LN2_LO = 0x1.a39ef35793c76p-33;
-  if (x != x) return x;
-  if (x < 0.0) return NAN;
-  if (x == 0.0) return -INFINITY;
-  if (x == INFINITY) return x;
-  uint64_t u = pht_d2u(x);
-  int k = 0;
-  if (u < 0x0010000000000000ULL) { /* subnormal */
-    x *= 18014398509481984.0;      /* 2^54 */
-    u = pht_d2u(x);
-    k = -54;
-  }
-  k += (int)(u >> 52) - 1023;
+  const int sub = (x < 0x1p-1022);                 /* subnormal (or <= 0) */
+  const double xs = sub ? x * 18014398509481984.0 : x; /* 2^54 */
+  const uint64_t u = pht_d2u(xs);
+  const int k0 = (int)((u >> 52) & 0x7ff) - 1023 - (sub ? 54 : 0);
   const uint64_t mant = u & 0x000fffffffffffffULL;
-  int idx = (int)(mant >> 45); /* top 7 bits */
-  uint64_t zb;
-  if (mant >= 0x6a09e667f3bcdULL) { /* m >= sqrt(2): z = m/2 */
-    zb = mant | 0x3fe0000000000000ULL;
-    k += 1;
-    idx += 128;
-  } else {
-    zb = mant | 0x3ff0000000000000ULL;
-  }
+  const int half = (mant >= 0x6a09e667f3bcdULL); /* m >= sqrt(2): z = m/2 */
+  const uint64_t zb = mant | (half ? 0x3fe0000000000000ULL : 0x3ff0000000000000ULL);
+  const int k = k0 + half;
+  const int idx = (int)(mant >> 45) + (half ? 128 : 0); /* top 7 bits */
   const double z = pht_u2d(zb);
-  const double invc = pht_log_tab[3 * idx], logc = pht_log_tab[3 * idx + 1], logclo = pht_log_tab[3 * idx + 2];
+  const double invc = PHT_LOG_TAB[3 * idx], logc = PHT_LOG_TAB[3 * idx + 1], logclo = PHT_LOG_TAB[3 * idx + 2];
   const double r = fma(z, invc, -1.0); /* |r| < 2^-7 */
   const double kd = (double)k;
   const double a = kd * LN2_HI;            /* exact */
@@ -447,7 +448,21 @@ PHT_HD double pht_log(double x) {
   q = fma(q, r, 0x1.5555555555555p-2);  /*  1/3 */
   q = fma(q, r, -0x1.0000000000000p-1); /* -1/2 */
   const double tail = fma(r * r, q, (lo + werr) + fma(kd, LN2_LO, logclo));
-  return hi + tail;
+  const double res = hi + tail;
+  /* specials: NaN -> NaN, x < 0 -> NaN, 0 -> -inf, +inf -> +inf */
+  const double spec = (x == 0.0) ? -INFINITY : ((x < 0.0) ? NAN : x);
+  return (x != x || x <= 0.0 || x == INFINITY) ? spec : res;
 }
+
+#if defined(__HIPCC__)
+/* copy the math tables into LDS (PHT_DETMATH_LDS); call at kernel entry,
+ * before the first __syncthreads() */
+__device__ __forceinline__ void pht_stage_math_tables() {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PHT_DETMATH_LDS)
+  for (int k = threadIdx.x; k < 128; k += blockDim.x) pht_lds_exp_tab[k] = pht_exp_tab[k];
+  for (int k = threadIdx.x; k < 768; k += blockDim.x) pht_lds_log_tab[k] = pht_log_tab[k];
+#endif
+}
+#endif
 
 #endif /* PHT_DETMATH_H */

@@ -551,11 +551,19 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
   double t = 0.0, d;
   int j = B, lastj;
   double p[ORC_MAXN + 1];
+#if ORC_DEV
+  /* device spec: the remaining time is carried as y_t <- y_t - d (the
+   * reference recomputes y - t); the exponentials of moveMass are then
+   * exactly those of the next absorb test, which the GPU reuses */
+  double yt = y;
+#endif
   for (int njump = 0;; njump++) {
 #if ORC_DEV
     if (njump >= ORC_MAX_JUMPS) { o->flags |= 8; break; }
-#endif
+    double y_t = yt;
+#else
     double y_t = y - t;
+#endif
     if (sp->s[j] > 0.0) {
       double U = ORC_FN(u)(rng), pab;
 #if ORC_DEV
@@ -587,6 +595,9 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
     /* LJMA_moveMass (:21-41) then the categorical draw (:352-358) */
     double x = y_t - d;
 #if ORC_DEV
+    yt = x;
+#endif
+#if ORC_DEV
     double E[ORC_MAXN], w[ORC_MAXN], sum = 0.0;
     const int *L = sp->succP + j * ORC_MAXN;
     const int cnt = sp->nsuccP[j];
@@ -613,7 +624,11 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
     o->N[lastj + j * n]++;
   }
   o->N[j + j * n]++;
+#if ORC_DEV
+  ORC_FN(zadd)(o, j, yt, zscale);
+#else
   ORC_FN(zadd)(o, j, y - t, zscale);
+#endif
   o->pre = j;
 }
 

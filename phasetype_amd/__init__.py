@@ -68,11 +68,14 @@ def load(build_if_needed: bool = True) -> C.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
-    if build_if_needed and _build.needs_build():
-        _build.build()
-    if not os.path.exists(_build.LIB):
-        raise PhaseTypeError(f"native library missing: {_build.LIB} (run phasetype_amd/build.py)")
-    L = C.CDLL(_build.LIB, mode=C.RTLD_LOCAL)
+    path = os.environ.get("PHT_LIB")  # a variant build (tools/ab.py)
+    if path is None:
+        if build_if_needed and _build.needs_build():
+            _build.build()
+        path = _build.LIB
+    if not os.path.exists(path):
+        raise PhaseTypeError(f"native library missing: {path} (run phasetype_amd/build.py)")
+    L = C.CDLL(path, mode=C.RTLD_LOCAL)
     L.pht_last_error.restype = C.c_char_p
     L.pht_bind_lapack.argtypes = [C.c_char_p, C.c_char_p]
     L.pht_set_seed.argtypes = [C.c_uint32]
@@ -119,11 +122,11 @@ def zexp_for(y) -> int:
 
 
 def stats_len(n: int) -> int:
-    return 2 * n + n * n + 8
+    return 2 * n + n * n + 16
 
 
 def split_stats(st, n):
-    """int64 block -> (zq[n], B[n], N[n,n] as N[from, to], extras[8])."""
+    """int64 block -> (zq[n], B[n], N[n,n] as N[from, to], extras[16])."""
     st = np.asarray(st)
     zq = st[:n]
     B = st[n:2 * n]

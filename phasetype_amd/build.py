@@ -20,6 +20,7 @@ LIB = os.path.join(OUT_DIR, "libPhaseType.so")
 SOURCES = ["pht_kernels.hip", "gibbs_host.cpp", "rstream.c"]
 HEADERS = ["pht_device.h", "pht_env.h", "pht_kernels.h", "pht_layout.h", "rstream.h"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+DEFAULT_DEFINES: tuple = ("PHT_DETMATH_LDS", "PHT_ENV_K=9")
 
 
 def _hipcc() -> str:
@@ -39,16 +40,19 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
+    """Compile; ``defines`` (e.g. ["PHT_DETMATH_LDS"]) and ``out`` build a
+    variant library elsewhere (tools/ab.py) without touching the default."""
+    target = out or LIB
+    if not force and not defines and out is None and not needs_build():
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
     objs = []
     for src in SOURCES:
         path = os.path.join(CSRC, src)
-        obj = os.path.join(OUT_DIR, src + ".o")
+        obj = os.path.join(OUT_DIR, os.path.basename(target) + "." + src + ".o")
         cmd = [_hipcc(), "-O3", "-fPIC", "-ffp-contract=off", f"-I{os.path.join(REPO, 'include')}", f"-I{CSRC}",
-               "-Wno-pass-failed"]
+               "-Wno-pass-failed"] + [f"-D{d}" for d in list(DEFAULT_DEFINES) + list(defines)]
         if src.endswith(".hip"):
             cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-std=c++17"]
         elif src.endswith(".cpp"):
@@ -60,13 +64,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = target + ".tmp"
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + ["-ldl"]
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, target)
     for o in objs:
         os.remove(o)
-    return LIB
+    return target
 
 
 if __name__ == "__main__":

@@ -92,6 +92,14 @@ struct Par {
 
 #define PHT_VEC(NT) ((NT) > 0 ? (NT) : kMaxN)
 
+/* division in the ARMS envelope code; PHT_FASTDIV_ABLATION is a timing-only
+ * diagnostic build (approximate reciprocal: results differ) */
+#ifdef PHT_FASTDIV_ABLATION
+#define PHT_DIV(a, b) ((a) * __builtin_amdgcn_rcp(b))
+#else
+#define PHT_DIV(a, b) ((a) / (b))
+#endif
+
 /* per-lane random stream helpers (oracle: orcD_u / orcD_runif / orcD_rexp) */
 __device__ __forceinline__ double dev_u(pht_stream &r) { return pht_next_u(&r); }
 __device__ __forceinline__ double dev_runif(pht_stream &r, double a, double b) {
@@ -111,7 +119,22 @@ struct Lane {
   int neval;
   int nbrent;
   int njump;
+#ifdef PHT_STAMPS
+  unsigned long long st_last, st_acc[8];
+#endif
 };
+
+/* diagnostic per-phase cycle stamps (wave-uniform s_memtime) */
+#ifdef PHT_STAMPS
+#define PHT_STAMP(ln, k)                                              \
+  do {                                                                \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();       \
+    (ln).st_acc[k] += t_ - (ln).st_last;                              \
+    (ln).st_last = t_;                                                \
+  } while (0)
+#else
+#define PHT_STAMP(ln, k) do { } while (0)
+#endif
 
 /* ===================================================================== ARMS */
 /* Envelope policies (pht_env.h) expose X/Y/CUM getters and sX/sY/sCUM
@@ -131,9 +154,9 @@ __device__ __forceinline__ void arms_meet(Env &e, int k) {
   double xm1 = 0.0, ym1 = 0.0, xp1 = 0.0, yp1 = 0.0;
   if (k >= 1) { xm1 = e.X(k - 1); ym1 = e.Y(k - 1); }
   if (k + 1 <= last) { xp1 = e.X(k + 1); yp1 = e.Y(k + 1); }
-  if (il) gl = (ym1 - e.Y(k - 3)) / (xm1 - e.X(k - 3));
-  if (ir) gr = (yp1 - e.Y(k + 3)) / (xp1 - e.X(k + 3));
-  if (irl) grl = (yp1 - ym1) / (xp1 - xm1);
+  if (il) gl = PHT_DIV((ym1 - e.Y(k - 3)), (xm1 - e.X(k - 3)));
+  if (ir) gr = PHT_DIV((yp1 - e.Y(k + 3)), (xp1 - e.X(k + 3)));
+  if (irl) grl = PHT_DIV((yp1 - ym1), (xp1 - xm1));
   if (irl && il && (gl < grl)) gl = gl + (1.0 + 1.0) * (grl - gl);
   if (irl && ir && (gr > grl)) gr = gr + (1.0 + 1.0) * (grl - gr);
   if (il && irl) {
@@ -145,8 +168,8 @@ __device__ __forceinline__ void arms_meet(Env &e, int k) {
     if (dl < kYEps) dl = kYEps;
   }
   if (il && ir && irl) {
-    e.sX(k, (dl * xp1 + dr * xm1) / (dl + dr));
-    e.sY(k, (dl * yp1 + dr * ym1 + dl * dr) / (dl + dr));
+    e.sX(k, PHT_DIV((dl * xp1 + dr * xm1), (dl + dr)));
+    e.sY(k, PHT_DIV((dl * yp1 + dr * ym1 + dl * dr), (dl + dr)));
   } else if (il && irl) {
     e.sX(k, xp1);
     e.sY(k, yp1 + dr);
@@ -176,9 +199,18 @@ __device__ __forceinline__ void arms_cumulate(Env &e) {
     const double xk = e.X(k), yk = e.Y(k);
     const double eyk = expshift(yk, ymax);
     double a;
+#ifdef PHT_AREA_SELECT
+    /* branch-free: both cheap forms, then select (same values) */
+    {
+      const double lin = 0.5 * (eyk + eyp) * (xk - xp);
+      const double ex = (PHT_DIV((eyk - eyp), (yk - yp))) * (xk - xp);
+      a = (xp == xk) ? 0. : ((fabs(yk - yp) < kYEps) ? lin : ex);
+    }
+#else
     if (xp == xk) a = 0.;
     else if (fabs(yk - yp) < kYEps) a = 0.5 * (eyk + eyp) * (xk - xp);
-    else a = ((eyk - eyp) / (yk - yp)) * (xk - xp);
+    else a = (PHT_DIV((eyk - eyp), (yk - yp))) * (xk - xp);
+#endif
     cum = cum + a;
     e.sCUM(k, cum);
     xp = xk; yp = yk; eyp = eyk;
@@ -202,7 +234,7 @@ __device__ __forceinline__ void arms_invert(Env &e, double prob, WPt &p) {
     cl = e.CUM(q - 1);
   }
   p.pr = q;
-  const double prop = (u - cl) / (cr - cl);
+  const double prop = PHT_DIV((u - cl), (cr - cl));
   const double xl = e.X(q - 1), xr = e.X(q);
   const double yr = e.Y(q);
   if (xl == xr) {
@@ -212,14 +244,14 @@ __device__ __forceinline__ void arms_invert(Env &e, double prob, WPt &p) {
   const double yl = e.Y(q - 1), eyl = expshift(yl, e.ymax), eyr = expshift(yr, e.ymax);
   if (fabs(yr - yl) < kYEps) {
     if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
-      p.x = xl + ((xr - xl) / (eyr - eyl)) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
+      p.x = xl + (PHT_DIV((xr - xl), (eyr - eyl))) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
     else
       p.x = xl + (xr - xl) * prop;
-    p.ey = ((p.x - xl) / (xr - xl)) * (eyr - eyl) + eyl;
+    p.ey = (PHT_DIV((p.x - xl), (xr - xl))) * (eyr - eyl) + eyl;
     p.y = logshift(p.ey, e.ymax);
   } else {
-    p.x = xl + ((xr - xl) / (yr - yl)) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
-    p.y = ((p.x - xl) / (xr - xl)) * (yr - yl) + yl;
+    p.x = xl + (PHT_DIV((xr - xl), (yr - yl))) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
+    p.y = (PHT_DIV((p.x - xl), (xr - xl))) * (yr - yl) + yl;
     p.ey = expshift(p.y, e.ymax);
   }
 }
@@ -279,6 +311,7 @@ __device__ __forceinline__ int arms(Env &e, const double xinit[4], double xl, do
   if ((xprev < xl) || (xprev > xr)) return 1007;
   const double yprev = f(xprev);
   ln.neval++;
+  PHT_STAMP(ln, 1);
   for (int it = 0;; it++) {
     if (it >= kArmsMaxIt) {
       xsamp = xprev;
@@ -300,7 +333,7 @@ __device__ __forceinline__ int arms(Env &e, const double xinit[4], double xl, do
     while (e.X(ql + 1) < xprev) ql++;
     const int qr = ql + 1;
     const double xql = e.X(ql), yql = e.Y(ql);
-    double w = (xprev - xql) / (e.X(qr) - xql);
+    double w = PHT_DIV((xprev - xql), (e.X(qr) - xql));
     double zold = yql + w * (e.Y(qr) - yql);
     double znew = p.y;
     if (yprev < zold) zold = yprev;
@@ -371,10 +404,10 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
  * into the reference's loop (src/Simulate_AbsCTMC_eq_Aslett_ECS.c:231-369). */
 template <int NT>
 struct EcsLane {
-  double y, t;
+  double yt;                 /* remaining time y - t, carried as yt <- yt - d (device spec) */
   int j, njump;
-  bool haveE0;               /* E0 valid for the current state and time */
-  double E0[PHT_VEC(NT)];    /* e^{λ_i (y - t)} from the absorb test */
+  bool haveE0;               /* E0 valid for the current remaining time */
+  double E0[PHT_VEC(NT)];    /* e^{λ_i yt}: absorb test / previous moveMass */
 };
 
 template <int NT, class Sink>
@@ -382,10 +415,10 @@ __device__ __forceinline__ void ecs_begin(const Par<NT> &P, double y, Lane &ln, 
   const double target = dev_u(ln.r);
   const int B = pistart(P, target, ln.flags);
   sk.start(B);
-  st.y = y;
-  st.t = 0.0;
+  st.yt = y;
   st.j = B;
   st.njump = 0;
+  st.haveE0 = false;
 }
 
 /* absorb test at the current state (LJMA_probAbsorb + runif, :251-255);
@@ -395,26 +428,26 @@ __device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink 
   const int n = P.n();
   const int j = st.j;
   bool fin = false;
-  st.haveE0 = false;
   if (st.njump >= kMaxJumps) {
     ln.flags |= kFlagJumpCap;
     fin = true;
   } else if (P.s(j) > 0.0) {
-    const double y_t = st.y - st.t;
+    const double y_t = st.yt;
     const double U = dev_u(ln.r);
+    if (!st.haveE0) {
+#pragma unroll
+      for (int i = 0; i < n; i++) st.E0[i] = pht_exp(P.evals(i) * y_t);
+      st.haveE0 = true;
+    }
     double den = 0.0;
 #pragma unroll
-    for (int i = 0; i < n; i++) {
-      st.E0[i] = pht_exp(P.evals(i) * y_t);
-      den = fma(P.QQs(j, i), st.E0[i], den);
-    }
-    st.haveE0 = true;
+    for (int i = 0; i < n; i++) den = fma(P.QQs(j, i), st.E0[i], den);
     const double pab = pht_exp(fma(P.S(j, j), y_t, P.logs(j)) - pht_log(den));
     fin = (U < pab);
   }
   if (fin) {
     sk.N(j, j);
-    sk.z(j, st.y - st.t);
+    sk.z(j, st.yt);
     sk.pre(j);
   }
   return fin;
@@ -426,9 +459,14 @@ template <int NT, class Env, class Sink>
 __device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st) {
   const int n = P.n();
   const int j = st.j;
-  const double y_t = st.y - st.t;
+  const double y_t = st.yt;
   const double Sjj = P.S(j, j);
-  EcsDens<NT> f{P, j, y_t, Sjj, st.E0, st.haveE0, -1.0, {}};
+  if (!st.haveE0) { /* s_j = 0: no absorb test ran at this state */
+#pragma unroll
+    for (int i = 0; i < n; i++) st.E0[i] = pht_exp(P.evals(i) * y_t);
+    st.haveE0 = true;
+  }
+  EcsDens<NT> f{P, j, y_t, Sjj, st.E0, true, -1.0, {}};
   double xinit[4];
   xinit[0] = (y_t) / 1e6;
   xinit[1] = (y_t) / 3.0;
@@ -436,23 +474,25 @@ __device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, S
   xinit[3] = y_t - xinit[0];
   double xsamp = 0.0;
   const int ainfo = arms(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln);
+  PHT_STAMP(ln, 2);
   if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
   const double d = xsamp;
-  st.t += d;
   const double x = y_t - d;
   /* e^{λ_i (y_t - d)}: the accepted proposal's density evaluation already
-   * computed them (d = lastd), or d = 0 = the absorb test's */
-  double E[PHT_VEC(NT)];
+   * computed them (d = lastd), or d = 0 = the absorb test's; they become
+   * the next absorb test's (yt <- x) */
+  double *E = st.E0;
   if (d == f.lastd) {
 #pragma unroll
     for (int i = 0; i < n; i++) E[i] = f.Elast[i];
-  } else if (d == 0.0 && st.haveE0) {
-#pragma unroll
-    for (int i = 0; i < n; i++) E[i] = st.E0[i];
+  } else if (d == 0.0) {
+    /* E0 already holds e^{λ_i y_t} = e^{λ_i x} */
   } else {
 #pragma unroll
     for (int i = 0; i < n; i++) E[i] = pht_exp(P.evals(i) * x);
   }
+  st.yt = x;
+  st.haveE0 = true;
   const int cnt = P.nsuccP(j);
   double w[PHT_VEC(NT)];
   double sum = 0.0;
@@ -490,6 +530,7 @@ __device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, S
   ln.njump++;
   st.njump++;
   st.j = nj;
+  PHT_STAMP(ln, 3);
 }
 
 template <int NT, class Env, class Sink>

@@ -77,6 +77,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
   PHT_LDS unsigned long long *xc = zq + n; /* kStatExtra counters */
   PHT_LDS unsigned *Bc = (PHT_LDS unsigned *)(xc + kStatExtra);
   PHT_LDS unsigned *Nc = Bc + n;
+  pht_stage_math_tables();
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
   __syncthreads();
@@ -152,7 +153,10 @@ static int smem_bytes(int n) {
  * all lanes of a wavefront active instead of waiting for the longest path.
  * The ARMS envelope lives in LDS (EnvLds<kEnvK>), lane-interleaved.
  */
-constexpr int kEnvK = 11;
+#ifndef PHT_ENV_K
+#define PHT_ENV_K 11
+#endif
+constexpr int kEnvK = PHT_ENV_K;
 
 template <int NT, bool DEBUG>
 __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
@@ -172,6 +176,7 @@ __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
   PHT_LDS unsigned *Nc = Bc + n;
   PHT_LDS int *cursor = (PHT_LDS int *)(Nc + n * n);
   PHT_LDS double *envl = (PHT_LDS double *)(lsm + ((pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 15) & ~15));
+  pht_stage_math_tables();
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
   if (threadIdx.x == 0) *cursor = 0;
@@ -186,20 +191,43 @@ __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
   env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill);
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
   Lane ln;
+#ifdef PHT_STAMPS
+  ln.st_last = __builtin_amdgcn_s_memtime();
+  for (int q = 0; q < 8; q++) ln.st_acc[q] = 0ull;
+#endif
   EcsLane<NT> st;
   long pos = 0;
   bool have = false, done = false;
+  /* the lane's next observation is claimed and its (y, gid) loaded one
+   * observation ahead, so a refill never waits on global memory */
+  auto claim = [&]() -> long {
+    return blockIdx.x +
+           (long)__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) * gridDim.x;
+  };
+  long nextp = claim();
+  double ny = 0.0;
+  uint32_t ngid = 0;
+  if (nextp < a.count) {
+    ny = a.y[a.begin + nextp];
+    ngid = a.gid[a.begin + nextp];
+  }
   for (;;) {
     bool need = false;
     while (!done) {
       if (!have) {
-        const long p = blockIdx.x + (long)__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) * gridDim.x;
-        if (p >= a.count) {
+        if (nextp >= a.count) {
           done = true;
           break;
         }
-        pos = a.begin + p;
-        pht_stream_init(&ln.r, a.k0, a.k1, a.gid[pos], 0u, a.sweep);
+        pos = a.begin + nextp;
+        const double yobs = ny;
+        const uint32_t gobs = ngid;
+        nextp = claim();
+        if (nextp < a.count) {
+          ny = a.y[a.begin + nextp];
+          ngid = a.gid[a.begin + nextp];
+        }
+        pht_stream_init(&ln.r, a.k0, a.k1, gobs, 0u, a.sweep);
         ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
         if (DEBUG) {
           sk.dz = a.dbg_zq + pos * n;
@@ -207,7 +235,7 @@ __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
           sk.dB = a.dbg_B + pos;
           sk.dpre = a.dbg_pre + pos;
         }
-        ecs_begin(P, a.y[pos], ln, sk, st);
+        ecs_begin(P, yobs, ln, sk, st);
         have = true;
       }
       if (ecs_try_absorb(P, ln, sk, st)) {
@@ -227,9 +255,14 @@ __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
       need = true;
       break;
     }
+    PHT_STAMP(ln, 0);
     if (!__any(need)) break;
     if (need) ecs_jump(P, ln, env, sk, st);
   }
+#ifdef PHT_STAMPS
+  if ((threadIdx.x & 63) == 0)
+    for (int q = 0; q < 4; q++) lds_add(&xc[8 + q], ln.st_acc[q]);
+#endif
   __syncthreads();
   unsigned long long *g = a.stats;
   for (int k = threadIdx.x; k < n; k += blockDim.x) {

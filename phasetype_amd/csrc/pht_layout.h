@@ -83,8 +83,9 @@ PHT_LHD Layout make_layout(int n) {
  *   [n, 2n)         B    start-state counts
  *   [2n, 2n+n^2)    N    N[i + j n] transitions i->j, diagonal = absorb-from
  *   then kStatExtra counters: obs processed, ARMS density evals, obs with
- *   flags, uniforms drawn, jumps, Brent CDF evals, overflow-replayed obs, spare */
-constexpr int kStatExtra = 8;
+ *   flags, uniforms drawn, jumps, Brent CDF evals, 2 spare, and 8 cycle
+ *   counters filled only by diagnostic PHT_STAMPS builds */
+constexpr int kStatExtra = 16; /* [8..15]: per-phase cycle stamps (PHT_STAMPS builds) */
 PHT_LHD int stats_len(int n) { return 2 * n + n * n + kStatExtra; }
 
 }  // namespace pht

@@ -1,0 +1,36 @@
+#!/usr/bin/env bash
+# Static ISA statistics of the sweep kernels (cross-compiled for gfx950, no GPU).
+# usage: tools/isa_stats.sh [extra hipcc -D flags ...]
+# Prints per-kernel VGPR/SGPR/scratch/LDS/occupancy and an opcode histogram
+# of the ECS exact kernel (top 30 opcodes).
+set -euo pipefail
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUT=${TMPDIR:-/tmp}/pht_isa
+mkdir -p "$OUT"
+cd "$OUT"
+/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -ffp-contract=off -Wno-pass-failed \
+  -DPHT_DETMATH_LDS -DPHT_ENV_K=9 "$@" -I"$ROOT/include" -I"$ROOT/phasetype_amd/csrc" \
+  --cuda-device-only -S -o k.s "$ROOT/phasetype_amd/csrc/pht_kernels.hip"
+python3 - k.s <<'EOF'
+import re, sys, collections
+s = open(sys.argv[1]).read()
+# resource usage comments emitted per function
+for blk in re.finditer(r"^(_Z\S+):[^\n]*\n(.*?)\.Lfunc_end", s, re.S | re.M):
+    name, body = blk.group(1), blk.group(2)
+    if "ecs_exact" not in name and "sweep_kernel" not in name:
+        continue
+    ops = collections.Counter()
+    for line in body.splitlines():
+        t = line.strip()
+        if not t or t.startswith((";", ".", "_", "s_nop")) or t.endswith(":"):
+            continue
+        ops[t.split()[0]] += 1
+    tot = sum(ops.values())
+    print(f"{name}: {tot} static insts")
+    if "ecs_exact" in name and "Lb0" in name:
+        for op, c in ops.most_common(30):
+            print(f"   {op:28s} {c}")
+for key in ("NumVgprs", "NumSgprs", "ScratchSize", "Occupancy", "LDSByteSize"):
+    vals = re.findall(rf"; {key}: (\d+)", s)
+    print(key, vals)
+EOF

@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Per-phase cycle breakdown of the ECS exact kernel from a PHT_STAMPS build
+(diagnostic only: stamps perturb the schedule; read shares, not totals).
+usage: PHT_LIB=/path/variant.so python3 tools/stamps.py [--N 1000000]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import phasetype_amd as P  # noqa: E402
+from phasetype_amd.synth import DATA_KEY, bd_exit, simulate_ph  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=10)
+ap.add_argument("--N", type=int, default=1_000_000)
+a = ap.parse_args()
+S, s = bd_exit(a.n)
+y, cen = simulate_ph(S, s, a.N, seed=DATA_KEY)
+sw = P.Sweeper(a.n, 2)
+sw.set_obs(y, cen)
+zexp = P.zexp_for(y)
+sw.sweep(S, s, zexp=zexp)
+st = sw.sweep(S, s, key=(3, 4), zexp=zexp)
+ex = st[2 * a.n + a.n * a.n:]
+names = ["phaseA_refill_absorb", "arms_init", "arms_loop", "movemass"]
+tot = float(sum(ex[8:12]))
+print(json.dumps({"kernel_ms": sw.last_kernel_ms(), "counters": ex[:8].tolist(),
+                  "shares": {k: float(v) / tot for k, v in zip(names, ex[8:12])},
+                  "evals_per_jump": float(ex[1]) / max(1, ex[4]), "jumps_per_obs": float(ex[4]) / a.N}, indent=1))
