@@ -32,6 +32,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 import phasetype_amd as P  # noqa: E402
+from phasetype_amd.dist import make_stats_allreduce, max_over_ranks, shard_range  # noqa: E402
 from phasetype_amd.synth import DATA_KEY, bd_exit, bd_exit_structure, simulate_ph  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
@@ -112,21 +113,14 @@ def main():
     nu, zeta = 1.0 + 50.0 * theta, np.full(m, 50.0)
     y, cen = simulate_ph(S, s, N, seed=DATA_KEY, censor_frac=args.censor)
     zexp = P.zexp_for(y)
-    lo, hi = N * rank // world, N * (rank + 1) // world
+    lo, hi = shard_range(N, rank, world)
     sw = P.Sweeper(n, method, 1, device=local)
     sw.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
     Cm = np.ones(T.shape)
 
     reduce = None
     if dist is not None:
-        import torch
-
-        buf = torch.zeros(P.stats_len(n), dtype=torch.int64, device=f"cuda:{local}")
-
-        def reduce(arr):  # noqa: F811
-            buf.copy_(torch.from_numpy(arr))
-            dist.all_reduce(buf)
-            arr[:] = buf.cpu().numpy()
+        reduce = make_stats_allreduce(dist, P.stats_len(n), device=f"cuda:{local}")
 
     def sync():
         if dist is not None:
@@ -145,11 +139,7 @@ def main():
     dt = time.perf_counter() - t0
     kernel_ms = sw.kernel_ms_total / args.steps
     if dist is not None:
-        import torch
-
-        t = torch.tensor([dt, kernel_ms], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, kernel_ms = float(t[0]), float(t[1])
+        dt, kernel_ms = max_over_ranks(dist, [dt, kernel_ms], device=f"cuda:{local}")
     if not np.all(np.isfinite(res)):
         raise SystemExit("non-finite Gibbs draws")
 

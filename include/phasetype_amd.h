@@ -16,7 +16,7 @@
  *    Aslett2,Hobolth2} occupy, src/PHT_MCMC_Aslett.c:325-333): one Gibbs
  *    step 1 over a shard of observations on one GPU, returning the int64
  *    sufficient-statistics block
- *      [zq n][B n][N n*n][8 counters]   (pht_stats_len(n) entries)
+ *      [zq n][B n][N n*n][16 counters]   (pht_stats_len(n) entries)
  *    zq = z in fixed point, z_k = zq_k * 2^-zexp; N[i + j n] = i->j
  *    transitions, diagonal = absorb-from counts (reference convention).
  *

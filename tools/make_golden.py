@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.npz from the reference's own C (oracle/_ref).
+
+Run here (where /root/reference exists): ``python tools/make_golden.py``.
+The fixtures hold inputs and outputs only (no reference source).  They pin the
+CPU restatement (oracle/, "ref" variant) wherever oracle/_ref is absent (the
+GPU box), per SURVEY.md §8(c) G1–G3:
+
+* G1 ``g1_test_scripts.npz`` — LJMA_Gibbs chains of the reference's two test
+  scripts, with the exact .C vectors of SURVEY.md §4.2 (tests/phtMCMC.R:1-22,
+  tests/phtMCMC2.R:1-21; their 20 observations are the scripts' own data).
+* G2 ``g2_cfg1.npz`` — config 1 (n=3 BD-exit, N=200 synthetic exact obs,
+  1000 sweeps) for ECS and MHRS.
+* G3 ``g3_sweeps.npz`` — one step-1 sweep, per observation (start state B,
+  z, N), for n in {3, 4, 10}, 100 exact + 100 censored observations, methods
+  MHRS (mhit 1 and 5), ECS, DCS, one R stream per case.
+"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from oracle import oracle as O  # noqa: E402
+from phasetype_amd.synth import bd_exit, bd_exit_structure, simulate_ph  # noqa: E402
+
+OUT = os.path.join(REPO, "tests", "golden")
+
+# the 20 observations of tests/phtMCMC.R:6-10 and tests/phtMCMC2.R:6-10
+X20 = np.array([
+    1.45353415045187, 1.85349532001349, 2.01084961814576, 0.505725921290172,
+    1.56252630012213, 3.41158665930278, 1.52674487509487, 4.3428662377235,
+    8.03208018151311, 2.41746547476986, 0.38828086509283, 2.61513815012196,
+    3.39148865480856, 1.82705817807965, 1.42090953713845, 0.851438991331866,
+    0.0178808867191894, 0.632198596390046, 0.959910259815998, 1.83344199966323])
+
+# .C vectors
+PHTMCMC2_ARGS = dict(seed=34752076, it=20, mhit=1, method=2, n=3, nu=[24.0, 180.0], zeta=[16.0, 16.0],
+                     T=[0, 2, 2, 0, 1, 0, 0, 0, 1, 0, 0, 0, 0, 1, 1, 0])
+# phtMCMC: names sorted in the C locale: S12 S13 S21 S23 S31 S32 s1 s2 s3
+#   T[i + 4 j] = index of the name at TT[i, j]
+_names = ["S12", "S13", "S21", "S23", "S31", "S32", "s1", "s2", "s3"]
+_nu_by = dict(zip(["S12", "S13", "s1", "S21", "S23", "s2", "S31", "S32", "s3"], [24, 24, 1, 180, 1, 24, 180, 1, 24]))
+_T1 = np.zeros((4, 4), np.int32)
+for i in range(3):
+    for j in range(3):
+        if i != j:
+            _T1[i, j] = _names.index(f"S{i + 1}{j + 1}") + 1
+    _T1[i, 3] = _names.index(f"s{i + 1}") + 1
+PHTMCMC_ARGS = dict(seed=576734884, it=6, mhit=1, method=1, n=3, nu=[float(_nu_by[k]) for k in _names],
+                    zeta=[16.0] * 9, T=list(_T1.reshape(-1, order="F")))
+
+
+def perturbed(n, seed):
+    S, s = bd_exit(n)
+    rng = np.random.default_rng(seed)
+    S = S.copy()
+    mask = S > 0
+    S[mask] *= rng.uniform(0.7, 1.3, mask.sum())
+    s = s * rng.uniform(0.7, 1.3, n)
+    np.fill_diagonal(S, 0.0)
+    np.fill_diagonal(S, -(S.sum(1) + s))
+    return S, s
+
+
+def g1(ref):
+    out = {"x": X20}
+    for tag, a in (("phtMCMC2", PHTMCMC2_ARGS), ("phtMCMC", PHTMCMC_ARGS)):
+        ref.set_seed(a["seed"])
+        m = len(a["nu"])
+        res = ref.gibbs(a["it"], a["mhit"], a["method"], a["n"], a["nu"], a["zeta"], np.array(a["T"], np.int32),
+                        np.ones(16), X20, np.zeros(20, np.int32), np.array([-1.0]), silent=1)
+        out[f"{tag}_res"] = res
+        for k in ("seed", "it", "mhit", "method", "n"):
+            out[f"{tag}_{k}"] = np.int64(a[k])
+        out[f"{tag}_nu"] = np.array(a["nu"])
+        out[f"{tag}_zeta"] = np.array(a["zeta"])
+        out[f"{tag}_T"] = np.array(a["T"], np.int32)
+        assert res.shape == (a["it"], m)
+    return out
+
+
+def g2(ref):
+    n, N, it = 3, 200, 1000
+    S, s = bd_exit(n)
+    T, theta = bd_exit_structure(n)
+    y, cen = simulate_ph(S, s, N, seed=0xC0F1, censor_frac=0.0)
+    nu, zeta = 1 + 50 * theta, np.full(len(theta), 50.0)
+    out = {"y": y, "T": T.reshape(-1, order="F").astype(np.int32), "nu": nu, "zeta": zeta, "n": np.int64(n),
+           "it": np.int64(it)}
+    for method, seed in ((2, 101), (1, 102)):
+        ref.set_seed(seed)
+        out[f"m{method}_seed"] = np.int64(seed)
+        out[f"m{method}_res"] = ref.gibbs(it, 1, method, n, nu, zeta, T.reshape(-1, order="F"), np.ones(T.size), y)
+    return out
+
+
+G3_CASES = [(n, method, mhit) for n in (3, 4, 10) for method, mhit in ((1, 1), (1, 5), (2, 1), (4, 1))]
+
+
+def g3(ref):
+    out = {}
+    for n in (3, 4, 10):
+        S0, s0 = bd_exit(n)
+        ye, _ = simulate_ph(S0, s0, 100, seed=500 + n, censor_frac=0.0)
+        yc, _ = simulate_ph(S0, s0, 100, seed=600 + n, censor_frac=0.0)
+        rng = np.random.default_rng(700 + n)
+        yc = yc * rng.uniform(0.05, 1.0, 100)  # right-censoring times
+        y = np.concatenate([ye, yc])
+        cen = np.concatenate([np.zeros(100, np.int32), np.ones(100, np.int32)])
+        S, s = perturbed(n, 800 + n)
+        out[f"n{n}_S"], out[f"n{n}_s"], out[f"n{n}_y"], out[f"n{n}_cen"] = S, s, y, cen
+    for i, (n, method, mhit) in enumerate(G3_CASES):
+        seed = 9000 + i
+        ref.set_seed(seed)
+        B, z, N = ref.sweep(method, out[f"n{n}_S"], out[f"n{n}_s"], out[f"n{n}_y"], out[f"n{n}_cen"], mhit=mhit,
+                            per_obs=True)
+        k = f"n{n}_m{method}_h{mhit}"
+        out[k + "_seed"] = np.int64(seed)
+        out[k + "_B"] = B.astype(np.int32)
+        out[k + "_z"] = z
+        out[k + "_N"] = N.astype(np.int16)
+    return out
+
+
+def main():
+    if not os.path.exists(O.REF_SO):
+        O.build(ref=True)
+    ref = O.RefLib()
+    os.makedirs(OUT, exist_ok=True)
+    for name, fn in (("g1_test_scripts", g1), ("g2_cfg1", g2), ("g3_sweeps", g3)):
+        d = fn(ref)
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), **d)
+        print(name, os.path.getsize(os.path.join(OUT, name + ".npz")), "bytes")
+
+
+if __name__ == "__main__":
+    main()
