@@ -147,14 +147,15 @@ def main():
         sweeps_per_s = args.steps / dt
         local_obs = hi - lo
         achieved = ALG_BYTES_PER_OBS * local_obs / (kernel_ms * 1e-3) / 1e9
-        traffic = None
+        traffic, flops = None, None
         if os.path.exists(args.traffic_file):
             try:
                 tf = json.load(open(args.traffic_file))
                 if tf.get("n") == n and tf.get("N_local") == local_obs and tf.get("method") == args.method:
                     traffic = tf.get("hbm_bytes_per_launch")
+                    flops = tf.get("fp64_flops_per_launch")
             except Exception:  # noqa: BLE001
-                traffic = None
+                traffic = flops = None
         line = {
             "metric": "Gibbs iterations/sec (whole node), n=10 states × N=1e6 observations",
             "value": sweeps_per_s,
@@ -178,6 +179,12 @@ def main():
                          "note": f"sweep kernel, {ALG_BYTES_PER_OBS} B/obs x {local_obs} obs per launch / "
                                  "HIP-event kernel time; the path is FP64-VALU/latency bound, see roofline_valu"},
         }
+        if flops:
+            tfs = flops / (kernel_ms * 1e-3) / 1e12
+            line["roofline_valu"] = {"bound": "fp64-valu", "achieved": tfs, "peak": FP64_VALU_PEAK_TF,
+                                     "unit": "TFLOP/s", "frac": tfs / FP64_VALU_PEAK_TF,
+                                     "note": "FP64 lane-flops per launch from PMC (SQ_INSTS_VALU_FLOPS_FP64 x 64 x "
+                                             "VALU lane utilisation, profiles/traffic_latest.json) / kernel time"}
         if world == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(n, y, cen, T, nu, zeta)

@@ -133,14 +133,32 @@ dgeevx_t p_dgeevx = nullptr;
 dgetrf_t p_dgetrf = nullptr;
 dgetri_t p_dgetri = nullptr;
 
-bool lapack_ready() {
-  if (p_dgeevx) return true;
-  /* inside R (or any process with an LP64 LAPACK loaded globally) */
-  p_dgeevx = (dgeevx_t)dlsym(RTLD_DEFAULT, "dgeevx_");
-  p_dgetrf = (dgetrf_t)dlsym(RTLD_DEFAULT, "dgetrf_");
-  p_dgetri = (dgetri_t)dlsym(RTLD_DEFAULT, "dgetri_");
+bool lookup_lapack(void *h) {
+  p_dgeevx = (dgeevx_t)dlsym(h, "dgeevx_");
+  p_dgetrf = (dgetrf_t)dlsym(h, "dgetrf_");
+  p_dgetri = (dgetri_t)dlsym(h, "dgetri_");
   if (p_dgeevx && p_dgetrf && p_dgetri) return true;
   p_dgeevx = nullptr;
+  return false;
+}
+
+bool lapack_ready() {
+  if (p_dgeevx) return true;
+  /* 1. an LP64 LAPACK in the global scope (e.g. R's own libRlapack) */
+  if (lookup_lapack(RTLD_DEFAULT)) return true;
+  /* 2. one this library was linked against (R loads package libraries
+   *    RTLD_LOCAL, so e.g. PKG_LIBS = $(LAPACK_LIBS) is only visible through
+   *    our own handle, which searches our dependency tree) */
+  Dl_info self{};
+  if (dladdr(reinterpret_cast<void *>(&pht_bind_lapack), &self) && self.dli_fname) {
+    void *h = dlopen(self.dli_fname, RTLD_LAZY | RTLD_NOLOAD);
+    if (h) {
+      const bool ok = lookup_lapack(h);
+      dlclose(h);
+      if (ok) return true;
+    }
+  }
+  /* 3. standalone: an explicit library (pht_bind_lapack or the environment) */
   const char *path = getenv("PHT_LAPACK_LIB");
   if (path) return pht_bind_lapack(path, getenv("PHT_LAPACK_PREFIX") ? getenv("PHT_LAPACK_PREFIX") : "") == 0;
   return false;

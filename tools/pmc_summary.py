@@ -40,17 +40,42 @@ def main(d, out=None, kernel_sub="pht::"):
         der["hbm_bytes_per_launch"] = der["hbm_read_bytes_corrected"] + der["hbm_write_bytes"]
     if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
         der["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(1.0, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+    if "SQ_INSTS_VALU_FLOPS_FP64" in avg and "valu_lane_utilization" in der:
+        # the counter advances once per wave instruction: x64 lanes x active-lane share
+        der["fp64_flops_per_launch"] = avg["SQ_INSTS_VALU_FLOPS_FP64"] * 64.0 * der["valu_lane_utilization"]
     if bench:
         kms = bench["roofline"]["kernel_ms"]
         der["kernel_ms_unprofiled_bench"] = kms
-        if "SQ_INSTS_VALU_FLOPS_FP64" in avg:
-            der["fp64_tflops_at_bench_time"] = avg["SQ_INSTS_VALU_FLOPS_FP64"] / (kms * 1e-3) / 1e12
+        if "fp64_flops_per_launch" in der:
+            der["fp64_tflops_at_bench_time"] = der["fp64_flops_per_launch"] / (kms * 1e-3) / 1e12
     res["derived"] = der
     js = json.dumps(res, indent=1, sort_keys=True)
     print(js)
     if out:
         open(out, "w").write(js)
+    return res, bench
+
+
+def write_traffic(res, bench, path, src):
+    """profiles/traffic_latest.json: read by bench.py as roofline.traffic when
+    its workload matches (n, local N, method)."""
+    der = res["derived"]
+    if "hbm_bytes_per_launch" not in der or not bench:
+        return
+    cfg = bench["config"]
+    t = {"n": cfg["n"], "N_local": cfg["N"] // bench["n_gpus"], "method": cfg["method"],
+         "hbm_bytes_per_launch": der["hbm_bytes_per_launch"],
+         "hbm_read_bytes_corrected": der.get("hbm_read_bytes_corrected"),
+         "hbm_write_bytes": der.get("hbm_write_bytes"),
+         "fp64_flops_per_launch": der.get("fp64_flops_per_launch"),
+         "kernel": "pht::ecs_exact_kernel (sum over the sweep's pht:: dispatches)",
+         "source": src,
+         "method_note": "FETCH_SIZE x 2 (gfx950 wide-read correction) x 1024 + WRITE_SIZE x 1024, "
+                        "per-dispatch averages from separate --pmc passes (MI355X_MICROARCH.md HBM)"}
+    open(path, "w").write(json.dumps(t, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    r, b = main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    if len(sys.argv) > 3:
+        write_traffic(r, b, sys.argv[3], sys.argv[1])
