@@ -123,18 +123,17 @@ __shared__ double pht_lds_log_tab[768];
 #define PHT_LOG_TAB pht_log_tab
 #endif
 
-PHT_HD double pht_exp(double x) {
-  /* straight-line (no branches: on the GPU every special case is a select) */
+/* Core of every exp below: e^x for |x| <= 709.78 with no special-case
+ * handling (callers guarantee the domain or select around it). */
+PHT_HD double pht_exp_core(double x) {
   const double INV_LN2_N = 0x1.71547652b82fep+6; /* 64/ln2 */
   const double LN2_HI_N = 0x1.62e42fefa39efp-7;  /* ln2/64 rounded */
   const double LN2_LO_N = 0x1.abc9e3b39803fp-62; /* ln2/64 - LN2_HI_N */
   const double SHIFT = 6755399441055744.0;       /* 1.5 * 2^52 */
-  const double HI = 709.782712893383973096, LO = -745.133219101941108420;
-  const double xc = (x > HI) ? HI : ((x < LO) ? LO : x); /* NaN passes through */
-  const double kd = fma(xc, INV_LN2_N, SHIFT) - SHIFT;   /* round-to-nearest-even integer */
-  double r = fma(-kd, LN2_HI_N, xc);
+  const double kd = fma(x, INV_LN2_N, SHIFT) - SHIFT; /* round-to-nearest-even integer */
+  double r = fma(-kd, LN2_HI_N, x);
   r = fma(-kd, LN2_LO_N, r); /* |r| <= ln2/128 */
-  const int ki = (xc == xc) ? (int)kd : 0;
+  const int ki = (int)kd;
   const int idx = ki & 63;
   const int k = ki >> 6; /* floor(ki / 64) */
   const double sc = PHT_EXP_TAB[2 * idx], tail = PHT_EXP_TAB[2 * idx + 1];
@@ -145,9 +144,30 @@ PHT_HD double pht_exp(double x) {
   q = fma(q, r, 0.5);
   const double p = fma(r * r, q, r); /* e^r - 1 */
   /* res * 2^k with one rounding (subnormal results) */
-  const double res = ldexp(sc + fma(sc, p, tail), k);
-  const double out = (x > HI) ? INFINITY : ((x < LO) ? 0.0 : res);
+  return ldexp(sc + fma(sc, p, tail), k);
+}
+
+#define PHT_EXP_HI 709.782712893383973096
+#define PHT_EXP_LO (-745.133219101941108420)
+
+/* e^x for every x: straight-line (selects, no branches on the GPU). */
+PHT_HD double pht_exp(double x) {
+  const double xc = fmin(fmax(x, PHT_EXP_LO), PHT_EXP_HI); /* NaN -> LO */
+  const double res = pht_exp_core(xc);
+  const double out = (x > PHT_EXP_HI) ? INFINITY : ((x < PHT_EXP_LO) ? 0.0 : res);
   return (x != x) ? x : out;
+}
+
+/* e^x for x >= LO (no underflow or NaN handling): pht_exp(x) there. */
+PHT_HD double pht_exp_hi(double x) {
+  const double res = pht_exp_core(fmin(x, PHT_EXP_HI));
+  return (x > PHT_EXP_HI) ? INFINITY : res;
+}
+
+/* e^x for x <= 709.78 (no overflow or NaN handling): pht_exp(x) there. */
+PHT_HD double pht_exp_neg(double x) {
+  const double res = pht_exp_core(fmax(x, PHT_EXP_LO));
+  return (x < PHT_EXP_LO) ? 0.0 : res;
 }
 
 /* log table, index i + 128 h (i = top 7 mantissa bits of m in [1,2), h = 1

@@ -40,6 +40,9 @@ double orc_norm_rand(void) { return pht_rs_norm_rand(&g_rs); }
 #undef ORC_FN
 #undef ORC_EXP
 #undef ORC_LOG
+#undef ORC_EXP_NEG
+#undef ORC_EXP_HI
+#undef ORC_EXP_CORE
 #define ORC_DEV 1
 #define ORC_FN(x) orcD_##x
 #include "pht_oracle_impl.h"

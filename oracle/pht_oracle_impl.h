@@ -50,6 +50,9 @@ static inline double ORC_FN(rexp)(ORC_FN(rng) *r, double scale) {
   return scale * -pht_log(pht_next_u(r));
 }
 #define ORC_EXP pht_exp
+#define ORC_EXP_NEG pht_exp_neg   /* arguments <= 0: spectral sums, stay-past-y */
+#define ORC_EXP_HI pht_exp_hi     /* arguments >= -50: expshift */
+#define ORC_EXP_CORE pht_exp_core /* arguments in (-50, 0]: Metropolis */
 #define ORC_LOG pht_log
 #else
 typedef pht_rstream ORC_FN(rng);
@@ -57,6 +60,9 @@ static inline double ORC_FN(u)(ORC_FN(rng) *r) { return pht_rs_unif_rand(r); }
 static inline double ORC_FN(runif)(ORC_FN(rng) *r, double a, double b) { return pht_rs_runif(r, a, b); }
 static inline double ORC_FN(rexp)(ORC_FN(rng) *r, double scale) { return pht_rs_rexp(r, scale); }
 #define ORC_EXP exp
+#define ORC_EXP_NEG exp
+#define ORC_EXP_HI exp
+#define ORC_EXP_CORE exp
 #define ORC_LOG log
 #endif
 
@@ -103,7 +109,7 @@ typedef struct {
 } ORC_FN(env);
 
 static inline double ORC_FN(expshift)(double y, double y0) {
-  return (y - y0 > -2.0 * ARMS_YCEIL) ? ORC_EXP(y - y0 + ARMS_YCEIL) : 0.0;
+  return (y - y0 > -2.0 * ARMS_YCEIL) ? ORC_EXP_HI(y - y0 + ARMS_YCEIL) : 0.0;
 }
 static inline double ORC_FN(logshift)(double y, double y0) { return ORC_LOG(y) + y0 - ARMS_YCEIL; }
 
@@ -281,7 +287,7 @@ static int ORC_FN(arms)(const double xinit[4], double xl, double xr, orc_dens f,
     if (ynew < znew) znew = ynew;
     w = ynew - znew - yold + zold;
     if (w > 0.0) w = 0.0;
-    w = (w > -ARMS_YCEIL) ? ORC_EXP(w) : 0.0;
+    w = (w > -ARMS_YCEIL) ? ORC_EXP_CORE(w) : 0.0;
     double um = ORC_FN(u)(rng);
     *xsamp = (um > w) ? e.xprev : p.x;
     if (neval_out) *neval_out += e.neval;
@@ -528,12 +534,12 @@ static double ORC_FN(ecs_dens)(double d, void *vctx) {
 #if ORC_DEV
   /* log(sum_i W[j,i] e^{lambda_i (y_t - d)}) + S_jj d */
   double x = c->y_t - d, acc = 0.0;
-  for (int i = 0; i < n; i++) acc = fma(sp->W[j + i * n], ORC_EXP(sp->evals[i] * x), acc);
+  for (int i = 0; i < n; i++) acc = fma(sp->W[j + i * n], ORC_EXP_NEG(sp->evals[i] * x), acc);
   return ORC_LOG(acc) + sp->S[j + j * n] * d;
 #else
   double pq[ORC_MAXN];
   ORC_FN(gemv_t)(n, sp->Q, c->p, pq);
-  for (int i = 0; i < n; i++) pq[i] *= ORC_EXP(sp->evals[i] * (c->y_t - d));
+  for (int i = 0; i < n; i++) pq[i] *= ORC_EXP_NEG(sp->evals[i] * (c->y_t - d));
   double term1 = 0.0;
   for (int i = 0; i < n; i++) term1 += pq[i] * sp->Qinv_s[i];
   return ORC_LOG(term1) + sp->S[j + j * n] * d;
@@ -568,13 +574,13 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
       double U = ORC_FN(u)(rng), pab;
 #if ORC_DEV
       double den = 0.0;
-      for (int i = 0; i < n; i++) den = fma(sp->QQs[j + i * n], ORC_EXP(sp->evals[i] * y_t), den);
+      for (int i = 0; i < n; i++) den = fma(sp->QQs[j + i * n], ORC_EXP_NEG(sp->evals[i] * y_t), den);
       pab = ORC_EXP(fma(sp->S[j + j * n], y_t, sp->logs[j]) - ORC_LOG(den));
 #else
       /* LJMA_probAbsorb (:120-136) */
       double num = (sp->S[j + j * n] * (y_t)) + log(sp->s[j]);
       double den = 0.0;
-      for (int i = 0; i < n; i++) den += sp->Q[j + i * n] * ORC_EXP(sp->evals[i] * (y_t)) * sp->Qinv_s[i];
+      for (int i = 0; i < n; i++) den += sp->Q[j + i * n] * ORC_EXP_NEG(sp->evals[i] * (y_t)) * sp->Qinv_s[i];
       pab = exp(num - log(den));
 #endif
       if (U < pab) break;
@@ -601,7 +607,7 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
     double E[ORC_MAXN], w[ORC_MAXN], sum = 0.0;
     const int *L = sp->succP + j * ORC_MAXN;
     const int cnt = sp->nsuccP[j];
-    for (int i = 0; i < n; i++) E[i] = ORC_EXP(sp->evals[i] * x);
+    for (int i = 0; i < n; i++) E[i] = ORC_EXP_NEG(sp->evals[i] * x);
     for (int q = 0; q < cnt; q++) {
       const int k = L[q];
       double acc = 0.0;
@@ -613,7 +619,7 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
     j = ORC_FN(catlist)(w, L, cnt, target, &o->flags);
 #else
     double tmp[ORC_MAXN], pp[ORC_MAXN], sum = 0.0;
-    for (int i = 0; i < n; i++) tmp[i] = ORC_EXP(sp->evals[i] * x) * sp->Qinv_s[i];
+    for (int i = 0; i < n; i++) tmp[i] = ORC_EXP_NEG(sp->evals[i] * x) * sp->Qinv_s[i];
     ORC_FN(gemv_n)(n, sp->Q, tmp, pp);
     for (int i = 0; i < n; i++) sum += pp[i] = pp[i] * sp->P[j + i * n];
     for (int i = 0; i < n; i++) pp[i] = pp[i] / sum;
@@ -647,7 +653,7 @@ static double ORC_FN(phtcdf)(const orc_sp *sp, double x, const double *pi) {
   double piQ[ORC_MAXN];
   ORC_FN(gemv_t)(n, sp->Q, pi, piQ);
   double r = 0.0;
-  for (int i = 0; i < n; i++) r += piQ[i] * ORC_EXP(x * sp->evals[i]) * sp->Qinv_1[i];
+  for (int i = 0; i < n; i++) r += piQ[i] * ORC_EXP_NEG(x * sp->evals[i]) * sp->Qinv_1[i];
   return r;
 }
 #endif
@@ -661,7 +667,7 @@ static double ORC_FN(cj_dens)(double d, void *vctx) {
 #if ORC_DEV
   if (x1 > 0) {
     double acc = 0.0;
-    for (int i = 0; i < n; i++) acc = fma(sp->V[j + i * n], ORC_EXP(sp->evals[i] * x1), acc);
+    for (int i = 0; i < n; i++) acc = fma(sp->V[j + i * n], ORC_EXP_NEG(sp->evals[i] * x1), acc);
     r1 = acc;
   } else {
     r1 = 1;
@@ -683,7 +689,7 @@ static double ORC_FN(condjump)(const orc_sp *sp, double tnow, int jnow, double y
   double x = y - tnow, denom;
 #if ORC_DEV
   double acc = 0.0;
-  for (int i = 0; i < n; i++) acc = fma(sp->QQ1[jnow + i * n], ORC_EXP(sp->evals[i] * x), acc);
+  for (int i = 0; i < n; i++) acc = fma(sp->QQ1[jnow + i * n], ORC_EXP_NEG(sp->evals[i] * x), acc);
   denom = acc;
 #else
   double pi[ORC_MAXN];
@@ -691,7 +697,7 @@ static double ORC_FN(condjump)(const orc_sp *sp, double tnow, int jnow, double y
   pi[jnow] = 1.0;
   denom = ORC_FN(phtcdf)(sp, x, pi);
 #endif
-  if (tnow < y && ORC_FN(runif)(rng, 0.0, 1.0) < ORC_EXP(sp->S[jnow + jnow * n] * (y - tnow)) / denom)
+  if (tnow < y && ORC_FN(runif)(rng, 0.0, 1.0) < ORC_EXP_NEG(sp->S[jnow + jnow * n] * (y - tnow)) / denom)
     return y - tnow + ORC_FN(rexp)(rng, 1.0 / -sp->S[jnow + jnow * n]);
   ORC_FN(cj_ctx) ctx = {sp, jnow, tnow, y};
   double xinit[4];
@@ -731,7 +737,7 @@ static void ORC_FN(obs_censored)(const orc_sp *sp, double y, int cens, ORC_FN(rn
       (void)sofar;
       const int *L = sp->succP + lastj * ORC_MAXN;
       const int cnt = sp->nsuccP[lastj];
-      for (int i = 0; i < n; i++) E[i] = ORC_EXP(sp->evals[i] * x1);
+      for (int i = 0; i < n; i++) E[i] = ORC_EXP_NEG(sp->evals[i] * x1);
       for (int i = 0; i < n; i++) r2 = fma(sp->V[lastj + i * n], E[i], r2);
       for (int q = 0; q < cnt; q++) {
         const int k = L[q];
@@ -801,12 +807,12 @@ static double ORC_FN(hobcdf)(double x, void *vctx) {
 #if ORC_DEV
     const double Ei = c->E[i];
 #else
-    const double Ei = ORC_EXP(sp->evals[i] * (c->y - c->t));
+    const double Ei = ORC_EXP_NEG(sp->evals[i] * (c->y - c->t));
 #endif
     if (fabs((sp->evals[i] - Sll) / Sll) < 1e-13)
       c->J[i] = x * Ei;
     else
-      c->J[i] = (Ei - ORC_EXP((c->y - c->t - x) * sp->evals[i] + Sll * x)) / (sp->evals[i] - Sll);
+      c->J[i] = (Ei - ORC_EXP_NEG((c->y - c->t - x) * sp->evals[i] + Sll * x)) / (sp->evals[i] - Sll);
   }
   double tmp = 0.0;
 #if ORC_DEV
@@ -876,7 +882,7 @@ static void ORC_FN(obs_dcs)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_ob
   double pend[ORC_MAXN], sum = 0.0;
 #if ORC_DEV
   double a[ORC_MAXN];
-  for (int i = 0; i < n; i++) a[i] = sp->piQ[i] * ORC_EXP(sp->evals[i] * y);
+  for (int i = 0; i < n; i++) a[i] = sp->piQ[i] * ORC_EXP_NEG(sp->evals[i] * y);
   for (int k = 0; k < n; k++) {
     double acc = 0.0;
     for (int i = 0; i < n; i++) acc = fma(a[i], sp->Qinv[i + k * n], acc);
@@ -889,7 +895,7 @@ static void ORC_FN(obs_dcs)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_ob
 #else
   double pq[ORC_MAXN], tmp[ORC_MAXN];
   ORC_FN(gemv_t)(n, sp->Q, sp->pi, pq);
-  for (int i = 0; i < n; i++) pq[i] *= ORC_EXP(sp->evals[i] * y);
+  for (int i = 0; i < n; i++) pq[i] *= ORC_EXP_NEG(sp->evals[i] * y);
   ORC_FN(gemv_t)(n, sp->Qinv, pq, tmp);
   for (int i = 0; i < n; i++) sum += pend[i] = tmp[i] * sp->s[i];
   for (int i = 0; i < n; i++) pend[i] = pend[i] / sum;
@@ -919,13 +925,13 @@ static void ORC_FN(obs_dcs)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_ob
     const double Sjj = sp->S[j + j * n];
 #if ORC_DEV
     double E[ORC_MAXN];
-    for (int i = 0; i < n; i++) E[i] = ORC_EXP(sp->evals[i] * x);
+    for (int i = 0; i < n; i++) E[i] = ORC_EXP_NEG(sp->evals[i] * x);
     for (int i = 0; i < n; i++) Pab = fma(sp->Q[j + i * n] * E[i], Qb[i], Pab);
 #else
-    for (int i = 0; i < n; i++) Pab += sp->Q[j + i * n] * ORC_EXP(sp->evals[i] * (y - t)) * Qb[i];
+    for (int i = 0; i < n; i++) Pab += sp->Q[j + i * n] * ORC_EXP_NEG(sp->evals[i] * (y - t)) * Qb[i];
 #endif
     if (bvec[j] > 0.0) {
-      if (ORC_FN(runif)(rng, 0.0, 1.0) < ORC_EXP(Sjj * (y - t)) / Pab) {
+      if (ORC_FN(runif)(rng, 0.0, 1.0) < ORC_EXP_NEG(Sjj * (y - t)) / Pab) {
         ORC_FN(zadd)(o, j, (y - t), zscale);
         o->N[j + j * n] = 1;
         o->pre = j;
@@ -935,10 +941,10 @@ static void ORC_FN(obs_dcs)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_ob
     for (int i = 0; i < n; i++) {
 #if ORC_DEV
       if (fabs((sp->evals[i] - Sjj) / Sjj) < 1e-13) J[i] = x * E[i];
-      else J[i] = (E[i] - ORC_EXP(Sjj * x)) / (sp->evals[i] - Sjj);
+      else J[i] = (E[i] - ORC_EXP_NEG(Sjj * x)) / (sp->evals[i] - Sjj);
 #else
-      if (fabs((sp->evals[i] - Sjj) / Sjj) < 1e-13) J[i] = (y - t) * ORC_EXP(sp->evals[i] * (y - t));
-      else J[i] = (ORC_EXP(sp->evals[i] * (y - t)) - ORC_EXP(Sjj * (y - t))) / (sp->evals[i] - Sjj);
+      if (fabs((sp->evals[i] - Sjj) / Sjj) < 1e-13) J[i] = (y - t) * ORC_EXP_NEG(sp->evals[i] * (y - t));
+      else J[i] = (ORC_EXP_NEG(sp->evals[i] * (y - t)) - ORC_EXP_NEG(Sjj * (y - t))) / (sp->evals[i] - Sjj);
 #endif
     }
     double p_sum = 0.0, prob;

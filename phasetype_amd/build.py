@@ -40,6 +40,12 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+def _merge_defines(defines) -> list:
+    """DEFAULT_DEFINES, with any macro that ``defines`` names replaced."""
+    names = {d.split("=")[0] for d in defines}
+    return [d for d in DEFAULT_DEFINES if d.split("=")[0] not in names] + list(defines)
+
+
 def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
     """Compile; ``defines`` (e.g. ["PHT_DETMATH_LDS"]) and ``out`` build a
     variant library elsewhere (tools/ab.py) without touching the default."""
@@ -52,7 +58,7 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
         path = os.path.join(CSRC, src)
         obj = os.path.join(OUT_DIR, os.path.basename(target) + "." + src + ".o")
         cmd = [_hipcc(), "-O3", "-fPIC", "-ffp-contract=off", f"-I{os.path.join(REPO, 'include')}", f"-I{CSRC}",
-               "-Wno-pass-failed"] + [f"-D{d}" for d in list(DEFAULT_DEFINES) + list(defines)]
+               "-Wno-pass-failed"] + [f"-D{d}" for d in _merge_defines(defines)]
         if src.endswith(".hip"):
             cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-std=c++17"]
         elif src.endswith(".cpp"):

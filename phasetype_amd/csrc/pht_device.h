@@ -142,7 +142,7 @@ struct Lane {
  * stored (the reference stores it, src/arms.c:19; recomputation from the
  * same y and ymax is bit-identical). */
 __device__ __forceinline__ double expshift(double y, double y0) {
-  return (y - y0 > -2.0 * kYCeil) ? pht_exp(y - y0 + kYCeil) : 0.0;
+  return (y - y0 > -2.0 * kYCeil) ? pht_exp_hi(y - y0 + kYCeil) : 0.0;
 }
 __device__ __forceinline__ double logshift(double y, double y0) { return pht_log(y) + y0 - kYCeil; }
 
@@ -289,30 +289,11 @@ __device__ __forceinline__ void arms_update(Env &e, const WPt &p, F &f, Lane &ln
   arms_cumulate(e);
 }
 
-/* arms() as used by the reference (xprev 0, one sample).  Returns 0, an
- * initial-point error code, or 4 on the iteration cap. */
+/* The sampling loop of arms() from iteration it0 on (src/arms.c:180-215:
+ * sample, test, update or Metropolis). */
 template <class Env, class F>
-__device__ __forceinline__ int arms(Env &e, const double xinit[4], double xl, double xr, F &f, double xprev, double &xsamp,
-                    Lane &ln) {
-  if ((xinit[0] <= xl) || (xinit[3] >= xr)) return 1003;
-  if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) return 1004;
-  e.cnt = 9;
-  e.sX(0, xl);
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    e.sX(2 * k + 1, xinit[k]);
-    e.sY(2 * k + 1, f(xinit[k]));
-  }
-  ln.neval += 4;
-  e.sX(8, xr);
-#pragma unroll
-  for (int k = 0; k < 9; k += 2) arms_meet(e, k);
-  arms_cumulate(e);
-  if ((xprev < xl) || (xprev > xr)) return 1007;
-  const double yprev = f(xprev);
-  ln.neval++;
-  PHT_STAMP(ln, 1);
-  for (int it = 0;; it++) {
+__device__ __forceinline__ int arms_loop(Env &e, F &f, double xprev, double yprev, double &xsamp, Lane &ln, int it0) {
+  for (int it = it0;; it++) {
     if (it >= kArmsMaxIt) {
       xsamp = xprev;
       return 4;
@@ -340,11 +321,240 @@ __device__ __forceinline__ int arms(Env &e, const double xinit[4], double xl, do
     if (ynew < znew) znew = ynew;
     w = ynew - znew - yprev + zold;
     if (w > 0.0) w = 0.0;
-    w = (w > -kYCeil) ? pht_exp(w) : 0.0;
+    w = (w > -kYCeil) ? pht_exp_core(w) : 0.0;
     const double um = dev_u(ln.r);
     xsamp = (um > w) ? xprev : p.x;
     return 0;
   }
+}
+
+/* arms() as used by the reference (xprev 0, one sample).  Returns 0, an
+ * initial-point error code, or 4 on the iteration cap. */
+template <class Env, class F>
+__device__ __forceinline__ int arms(Env &e, const double xinit[4], double xl, double xr, F &f, double xprev, double &xsamp,
+                    Lane &ln) {
+  if ((xinit[0] <= xl) || (xinit[3] >= xr)) return 1003;
+  if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) return 1004;
+  e.cnt = 9;
+  e.sX(0, xl);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    e.sX(2 * k + 1, xinit[k]);
+    e.sY(2 * k + 1, f(xinit[k]));
+  }
+  ln.neval += 4;
+  e.sX(8, xr);
+#pragma unroll
+  for (int k = 0; k < 9; k += 2) arms_meet(e, k);
+  arms_cumulate(e);
+  if ((xprev < xl) || (xprev > xr)) return 1007;
+  const double yprev = f(xprev);
+  ln.neval++;
+  PHT_STAMP(ln, 1);
+  return arms_loop(e, f, xprev, yprev, xsamp, ln, 0);
+}
+
+/* ------------------------------------------------ register fast path */
+/* The freshly initialised envelope always has 9 points at fixed positions
+ * (bound, 4 evaluated points, 4 intersections).  Env9 holds them in
+ * registers: meet/cumulate/invert/Metropolis run with compile-time indices
+ * (selects instead of LDS or scratch traffic), ey is computed once per point
+ * in cumulate and reused by invert (same value: same expression, same
+ * operands).  Only a rejected first proposal (an envelope update, ~10 % of
+ * ECS sojourns) copies the points into a general envelope and continues in
+ * arms_loop().  Every arithmetic step is the one of arms_meet /
+ * arms_cumulate / arms_invert / arms_loop, so results are identical. */
+struct Env9 {
+  double x[9], y[9], cum[9], ymax;
+#ifndef PHT_ENV9_LEAN
+  double ey[9];
+#endif
+};
+
+template <int K>
+__device__ __forceinline__ void env9_meet(Env9 &e) {
+  constexpr int last = 8;
+  constexpr bool il = (K >= 3), ir = (K + 3 <= last), irl = (K >= 1 && K + 1 <= last);
+  double gl = 0.0, gr = 0.0, grl = 0.0, dl = 0.0, dr = 0.0;
+  double xm1 = 0.0, ym1 = 0.0, xp1 = 0.0, yp1 = 0.0;
+  if constexpr (K >= 1) { xm1 = e.x[K - 1]; ym1 = e.y[K - 1]; }
+  if constexpr (K + 1 <= last) { xp1 = e.x[K + 1]; yp1 = e.y[K + 1]; }
+  if constexpr (il) gl = PHT_DIV((ym1 - e.y[K - 3]), (xm1 - e.x[K - 3]));
+  if constexpr (ir) gr = PHT_DIV((yp1 - e.y[K + 3]), (xp1 - e.x[K + 3]));
+  if constexpr (irl) grl = PHT_DIV((yp1 - ym1), (xp1 - xm1));
+  if constexpr (irl && il) gl = (gl < grl) ? gl + (1.0 + 1.0) * (grl - gl) : gl;
+  if constexpr (irl && ir) gr = (gr > grl) ? gr + (1.0 + 1.0) * (grl - gr) : gr;
+  if constexpr (il && irl) {
+    dr = (gl - grl) * (xp1 - xm1);
+    dr = (dr < kYEps) ? kYEps : dr;
+  }
+  if constexpr (ir && irl) {
+    dl = (grl - gr) * (xp1 - xm1);
+    dl = (dl < kYEps) ? kYEps : dl;
+  }
+  if constexpr (il && ir && irl) {
+    e.x[K] = PHT_DIV((dl * xp1 + dr * xm1), (dl + dr));
+    e.y[K] = PHT_DIV((dl * yp1 + dr * ym1 + dl * dr), (dl + dr));
+  } else if constexpr (il && irl) {
+    e.x[K] = xp1;
+    e.y[K] = yp1 + dr;
+  } else if constexpr (ir && irl) {
+    e.x[K] = xm1;
+    e.y[K] = ym1 + dl;
+  } else if constexpr (il) {
+    e.y[K] = ym1 + gl * (e.x[K] - xm1);
+  } else if constexpr (ir) {
+    e.y[K] = yp1 - gr * (xp1 - e.x[K]);
+  }
+}
+
+__device__ __forceinline__ void env9_cumulate(Env9 &e) {
+  double ymax = e.y[0];
+#pragma unroll
+  for (int k = 1; k < 9; k++) ymax = (e.y[k] > ymax) ? e.y[k] : ymax;
+  e.ymax = ymax;
+#ifdef PHT_ENV9_LEAN
+  double ey[9];
+#else
+  double *ey = e.ey;
+#endif
+#pragma unroll
+  for (int k = 0; k < 9; k++) ey[k] = expshift(e.y[k], ymax);
+  double cum = 0.;
+  e.cum[0] = cum;
+#pragma unroll
+  for (int k = 1; k < 9; k++) {
+    const double xp = e.x[k - 1], xk = e.x[k], yp = e.y[k - 1], yk = e.y[k];
+    const double lin = 0.5 * (ey[k] + ey[k - 1]) * (xk - xp);
+    const double ex = (PHT_DIV((ey[k] - ey[k - 1]), (yk - yp))) * (xk - xp);
+    const double a = (xp == xk) ? 0. : ((fabs(yk - yp) < kYEps) ? lin : ex);
+    cum = cum + a;
+    e.cum[k] = cum;
+  }
+}
+
+/* arms_invert on Env9: the segment scan runs top-down with selects */
+__device__ __forceinline__ void env9_invert(const Env9 &e, double prob, WPt &p) {
+  const double u = prob * e.cum[8];
+  int q = 8;
+  double cl = e.cum[7], cr = e.cum[8];
+  double xl = e.x[7], xr = e.x[8], yl = e.y[7], yr = e.y[8];
+#ifndef PHT_ENV9_LEAN
+  double eyl = e.ey[7], eyr = e.ey[8];
+#endif
+  bool go = true;
+#pragma unroll
+  for (int k = 7; k >= 1; k--) {
+    go = go && (cl > u); /* cl == cum[k] here */
+    if (go) {
+      q = k;
+      cr = e.cum[k]; cl = e.cum[k - 1];
+      xr = e.x[k]; xl = e.x[k - 1];
+      yr = e.y[k]; yl = e.y[k - 1];
+#ifndef PHT_ENV9_LEAN
+      eyr = e.ey[k]; eyl = e.ey[k - 1];
+#endif
+    }
+  }
+#ifdef PHT_ENV9_LEAN
+  const double eyl = expshift(yl, e.ymax), eyr = expshift(yr, e.ymax);
+#endif
+  p.pr = q;
+  const double prop = PHT_DIV((u - cl), (cr - cl));
+  if (xl == xr) {
+    p.x = xr; p.y = yr; p.ey = eyr;
+    return;
+  }
+  if (fabs(yr - yl) < kYEps) {
+    if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
+      p.x = xl + (PHT_DIV((xr - xl), (eyr - eyl))) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
+    else
+      p.x = xl + (xr - xl) * prop;
+    p.ey = (PHT_DIV((p.x - xl), (xr - xl))) * (eyr - eyl) + eyl;
+    p.y = logshift(p.ey, e.ymax);
+  } else {
+    p.x = xl + (PHT_DIV((xr - xl), (yr - yl))) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
+    p.y = (PHT_DIV((p.x - xl), (xr - xl))) * (yr - yl) + yl;
+    p.ey = expshift(p.y, e.ymax);
+  }
+}
+
+/* arms() with the first iteration on Env9; `slow` is the general envelope
+ * used only after a rejection.  Same draws, evaluations and results. */
+template <class Env, class F>
+__device__ __forceinline__ int arms_fast(Env &slow, const double xinit[4], double xl, double xr, F &f, double xprev,
+                                         double &xsamp, Lane &ln) {
+  if ((xinit[0] <= xl) || (xinit[3] >= xr)) return 1003;
+  if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) return 1004;
+  Env9 e;
+  e.x[0] = xl;
+  e.y[0] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    e.x[2 * k + 1] = xinit[k];
+    e.y[2 * k + 1] = f(xinit[k]);
+    e.x[2 * k + 2] = 0.0;
+    e.y[2 * k + 2] = 0.0;
+  }
+  ln.neval += 4;
+  e.x[8] = xr;
+  env9_meet<0>(e);
+  env9_meet<2>(e);
+  env9_meet<4>(e);
+  env9_meet<6>(e);
+  env9_meet<8>(e);
+  env9_cumulate(e);
+  if ((xprev < xl) || (xprev > xr)) return 1007;
+  const double yprev = f(xprev);
+  ln.neval++;
+  PHT_STAMP(ln, 1);
+  /* iteration 0 (arms_loop body) */
+  WPt p;
+  env9_invert(e, dev_u(ln.r), p);
+  const double u = dev_u(ln.r) * p.ey;
+  const double yv = logshift(u, e.ymax);
+  const double ynew = f(p.x);
+  ln.neval++;
+  if (yv >= ynew) {
+    /* rejected: hand the envelope to the general code */
+    slow.cnt = 9;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      slow.sX(k, e.x[k]);
+      slow.sY(k, e.y[k]);
+      slow.sCUM(k, e.cum[k]);
+    }
+    slow.ymax = e.ymax;
+    p.y = ynew;
+    p.ey = expshift(p.y, e.ymax);
+    arms_update(slow, p, f, ln);
+    return arms_loop(slow, f, xprev, yprev, xsamp, ln, 1);
+  }
+  /* Metropolis step: ql = first k with x[k+1] >= xprev */
+  int ql = 0;
+  double xql = e.x[0], yql = e.y[0], xqr = e.x[1], yqr = e.y[1];
+  bool go = true;
+#pragma unroll
+  for (int k = 1; k < 8; k++) {
+    go = go && (xqr < xprev); /* xqr == x[k] here */
+    if (go) {
+      ql = k;
+      xql = e.x[k]; yql = e.y[k];
+      xqr = e.x[k + 1]; yqr = e.y[k + 1];
+    }
+  }
+  (void)ql;
+  double w = PHT_DIV((xprev - xql), (xqr - xql));
+  double zold = yql + w * (yqr - yql);
+  double znew = p.y;
+  if (yprev < zold) zold = yprev;
+  if (ynew < znew) znew = ynew;
+  w = ynew - znew - yprev + zold;
+  if (w > 0.0) w = 0.0;
+  w = (w > -kYCeil) ? pht_exp_core(w) : 0.0;
+  const double um = dev_u(ln.r);
+  xsamp = (um > w) ? xprev : p.x;
+  return 0;
 }
 
 /* ====================================================== categorical scans */
@@ -390,7 +600,7 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
     } else {
 #pragma unroll
       for (int i = 0; i < n; i++) {
-        Elast[i] = pht_exp(P.evals(i) * x);
+        Elast[i] = pht_exp_neg(P.evals(i) * x);
         acc = fma(P.W(j, i), Elast[i], acc);
       }
     }
@@ -436,7 +646,7 @@ __device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink 
     const double U = dev_u(ln.r);
     if (!st.haveE0) {
 #pragma unroll
-      for (int i = 0; i < n; i++) st.E0[i] = pht_exp(P.evals(i) * y_t);
+      for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
       st.haveE0 = true;
     }
     double den = 0.0;
@@ -463,7 +673,7 @@ __device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, S
   const double Sjj = P.S(j, j);
   if (!st.haveE0) { /* s_j = 0: no absorb test ran at this state */
 #pragma unroll
-    for (int i = 0; i < n; i++) st.E0[i] = pht_exp(P.evals(i) * y_t);
+    for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
     st.haveE0 = true;
   }
   EcsDens<NT> f{P, j, y_t, Sjj, st.E0, true, -1.0, {}};
@@ -473,7 +683,11 @@ __device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, S
   xinit[2] = xinit[1] * 2.0;
   xinit[3] = y_t - xinit[0];
   double xsamp = 0.0;
+#ifdef PHT_ECS_NOFAST
   const int ainfo = arms(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln);
+#else
+  const int ainfo = arms_fast(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln);
+#endif
   PHT_STAMP(ln, 2);
   if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
   const double d = xsamp;
@@ -489,7 +703,7 @@ __device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, S
     /* E0 already holds e^{λ_i y_t} = e^{λ_i x} */
   } else {
 #pragma unroll
-    for (int i = 0; i < n; i++) E[i] = pht_exp(P.evals(i) * x);
+    for (int i = 0; i < n; i++) E[i] = pht_exp_neg(P.evals(i) * x);
   }
   st.yt = x;
   st.haveE0 = true;
@@ -553,7 +767,7 @@ struct CjDens { /* log F_{P_j}(y - t - d) + log dexp(d; 1/-S_jj) */
     if (x1 > 0) {
       double acc = 0.0;
 #pragma unroll
-      for (int i = 0; i < n; i++) acc = fma(P.V(j, i), pht_exp(P.evals(i) * x1), acc);
+      for (int i = 0; i < n; i++) acc = fma(P.V(j, i), pht_exp_neg(P.evals(i) * x1), acc);
       r1 = acc;
     } else {
       r1 = 1;
@@ -586,8 +800,8 @@ __device__ __forceinline__ void censored(const Par<NT> &P, double y, Lane &ln, E
       const double x = y - t;
       double denom = 0.0;
 #pragma unroll
-      for (int i = 0; i < n; i++) denom = fma(P.QQ1(j, i), pht_exp(P.evals(i) * x), denom);
-      if (t < y && dev_runif(ln.r, 0.0, 1.0) < pht_exp(Sjj * (y - t)) / denom) {
+      for (int i = 0; i < n; i++) denom = fma(P.QQ1(j, i), pht_exp_neg(P.evals(i) * x), denom);
+      if (t < y && dev_runif(ln.r, 0.0, 1.0) < pht_exp_neg(Sjj * (y - t)) / denom) {
         d = y - t + dev_rexp(ln.r, 1.0 / -Sjj);
       } else {
         CjDens<NT> f{P, j, t, y, P.scale(j), P.logscale(j)};
@@ -608,7 +822,7 @@ __device__ __forceinline__ void censored(const Par<NT> &P, double y, Lane &ln, E
       const double x1 = y - t;
       double E[PHT_VEC(NT)];
 #pragma unroll
-      for (int i = 0; i < n; i++) E[i] = pht_exp(P.evals(i) * x1);
+      for (int i = 0; i < n; i++) E[i] = pht_exp_neg(P.evals(i) * x1);
       double r2 = 0.0;
 #pragma unroll
       for (int i = 0; i < n; i++) r2 = fma(P.V(lastj, i), E[i], r2);
@@ -792,7 +1006,7 @@ struct HobCdf {
       const double ev = P.evals(i), Ei = E[i];
       double Ji;
       if (fabs((ev - Sll) / Sll) < 1e-13) Ji = x * Ei;
-      else Ji = (Ei - pht_exp((y - t - x) * ev + Sll * x)) / (ev - Sll);
+      else Ji = (Ei - pht_exp_neg((y - t - x) * ev + Sll * x)) / (ev - Sll);
       tmp = fma(P.Q(j, i) * Ji, Qb[i], tmp);
     }
     return 1 / prob * P.S(lastj, j) / Pab * tmp - u;
@@ -855,7 +1069,7 @@ __device__ __forceinline__ void dcs(const Par<NT> &P, double y, Lane &ln, Sink &
   /* end state b ~ (pi e^{yS})_b s_b */
   double a[PHT_VEC(NT)];
 #pragma unroll
-  for (int i = 0; i < n; i++) a[i] = P.piQ(i) * pht_exp(P.evals(i) * y);
+  for (int i = 0; i < n; i++) a[i] = P.piQ(i) * pht_exp_neg(P.evals(i) * y);
   int b;
   {
     double pend[PHT_VEC(NT)], sum = 0.0;
@@ -898,12 +1112,12 @@ __device__ __forceinline__ void dcs(const Par<NT> &P, double y, Lane &ln, Sink &
     const double Sjj = P.S(j, j);
     double E[PHT_VEC(NT)];
 #pragma unroll
-    for (int i = 0; i < n; i++) E[i] = pht_exp(P.evals(i) * x);
+    for (int i = 0; i < n; i++) E[i] = pht_exp_neg(P.evals(i) * x);
     double Pab = 0.0;
 #pragma unroll
     for (int i = 0; i < n; i++) Pab = fma(P.Q(j, i) * E[i], Qb[i], Pab);
     if (j == b) {
-      if (dev_runif(ln.r, 0.0, 1.0) < pht_exp(Sjj * (y - t)) / Pab) {
+      if (dev_runif(ln.r, 0.0, 1.0) < pht_exp_neg(Sjj * (y - t)) / Pab) {
         sk.z(j, (y - t));
         sk.N(j, j);
         sk.pre(j);
@@ -915,7 +1129,7 @@ __device__ __forceinline__ void dcs(const Par<NT> &P, double y, Lane &ln, Sink &
     for (int i = 0; i < n; i++) {
       const double ev = P.evals(i);
       if (fabs((ev - Sjj) / Sjj) < 1e-13) J[i] = x * E[i];
-      else J[i] = (E[i] - pht_exp(Sjj * x)) / (ev - Sjj);
+      else J[i] = (E[i] - pht_exp_neg(Sjj * x)) / (ev - Sjj);
     }
     const int cnt = P.nsuccS(j);
     double pw[PHT_VEC(NT)];

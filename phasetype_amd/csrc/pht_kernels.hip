@@ -158,8 +158,15 @@ static int smem_bytes(int n) {
 #endif
 constexpr int kEnvK = PHT_ENV_K;
 
+#ifndef PHT_ECS_WAVES
+#define PHT_ECS_WAVES 0
+#endif
 template <int NT, bool DEBUG>
-__global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
+__global__ void __launch_bounds__(kBlock)
+#if PHT_ECS_WAVES > 0
+__attribute__((amdgpu_waves_per_eu(PHT_ECS_WAVES, PHT_ECS_WAVES)))
+#endif
+ecs_exact_kernel(SweepArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
   const Layout L = make_layout(n);
@@ -186,9 +193,16 @@ __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
   P.d = (const PHT_LDS double *)lsm;
   P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
   P.Lr = L;
+#ifdef PHT_ECS_NOFAST
   EnvLds<kEnvK, kBlock> env;
   double spill[3 * EnvLds<kEnvK, kBlock>::kSpill];
   env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill);
+#else
+  /* fresh envelopes live in registers (arms_fast); this one only takes the
+   * rarely updated ones */
+  (void)envl;
+  EnvPrivate env;
+#endif
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
   Lane ln;
 #ifdef PHT_STAMPS
@@ -276,7 +290,11 @@ __global__ void __launch_bounds__(kBlock) ecs_exact_kernel(SweepArgs a) {
 }
 
 static int smem_bytes_ecs(int n) {
+#ifdef PHT_ECS_NOFAST
   return ((smem_bytes(n) + 4 + 15) & ~15) + EnvLds<kEnvK, kBlock>::lds_doubles_per_lane() * 8 * kBlock;
+#else
+  return (smem_bytes(n) + 4 + 15) & ~15;
+#endif
 }
 
 template <int NT, bool DEBUG>
