@@ -183,8 +183,49 @@ __device__ __forceinline__ void arms_meet(Env &e, int k) {
   }
 }
 
+/* Envelopes of up to kArmsU points (the initial 9 plus two updates) use
+ * fixed-trip unrolled loops: every access has a compile-time position, so
+ * the loads issue together instead of one dependent load per iteration.
+ * Positions >= cnt hold stale values that are read and then discarded by
+ * selects, or written where no live point is; results are those of the
+ * rolled loops. */
+constexpr int kArmsU = 13;
+
+template <class Env>
+__device__ __forceinline__ void arms_cumulate_u(Env &e) {
+  const int cnt = e.cnt;
+  double xs[kArmsU], ys[kArmsU];
+#pragma unroll
+  for (int k = 0; k < kArmsU; k++) {
+    xs[k] = e.X(k);
+    ys[k] = e.Y(k);
+  }
+  double ymax = ys[0];
+#pragma unroll
+  for (int k = 1; k < kArmsU; k++) ymax = (k < cnt && ys[k] > ymax) ? ys[k] : ymax;
+  e.ymax = ymax;
+  double eyp = expshift(ys[0], ymax);
+  double cum = 0.;
+  e.sCUM(0, cum);
+#pragma unroll
+  for (int k = 1; k < kArmsU; k++) {
+    const double xp = xs[k - 1], xk = xs[k], yp = ys[k - 1], yk = ys[k];
+    const double eyk = expshift(yk, ymax);
+    const double lin = 0.5 * (eyk + eyp) * (xk - xp);
+    const double ex = (PHT_DIV((eyk - eyp), (yk - yp))) * (xk - xp);
+    const double a = (xp == xk) ? 0. : ((fabs(yk - yp) < kYEps) ? lin : ex);
+    cum = cum + a;
+    e.sCUM(k, cum);
+    eyp = eyk;
+  }
+}
+
 template <class Env>
 __device__ __forceinline__ void arms_cumulate(Env &e) {
+  if (e.cnt <= kArmsU) {
+    arms_cumulate_u(e);
+    return;
+  }
   double ymax = e.Y(0);
   for (int k = 1; k < e.cnt; k++) {
     const double yk = e.Y(k);
@@ -226,12 +267,32 @@ template <class Env>
 __device__ __forceinline__ void arms_invert(Env &e, double prob, WPt &p) {
   int q = e.cnt - 1;
   const double u = prob * e.CUM(q);
-  const double cr0 = e.CUM(q);
-  double cl = e.CUM(q - 1), cr = cr0;
-  while (cl > u) {
-    q--;
-    cr = cl;
+  double cl, cr;
+  if (e.cnt <= kArmsU) {
+    /* q moves down from last while cum[q-1] > u (scan unrolled) */
+    const int last = e.cnt - 1;
+    double cs[kArmsU];
+#pragma unroll
+    for (int k = 0; k < kArmsU; k++) cs[k] = e.CUM(k);
+    bool go = true;
+#pragma unroll
+    for (int k = kArmsU - 2; k >= 1; k--) {
+      if (k <= last - 1) {
+        go = go && (cs[k] > u);
+        q = go ? k : q;
+      }
+    }
+    cr = e.CUM(q);
     cl = e.CUM(q - 1);
+  } else {
+    const double cr0 = e.CUM(q);
+    cl = e.CUM(q - 1);
+    cr = cr0;
+    while (cl > u) {
+      q--;
+      cr = cl;
+      cl = e.CUM(q - 1);
+    }
   }
   p.pr = q;
   const double prop = PHT_DIV((u - cl), (cr - cl));
@@ -260,9 +321,26 @@ template <class Env, class F>
 __device__ __forceinline__ void arms_update(Env &e, const WPt &p, F &f, Lane &ln) {
   if (e.cnt > kArmsNPoint - 2) return;
   const int pr = p.pr;
-  for (int k = e.cnt - 1; k >= pr; k--) {
-    e.sX(k + 2, e.X(k));
-    e.sY(k + 2, e.Y(k));
+  if (e.cnt <= kArmsU) {
+    /* positions pr..cnt-1 move up by 2: read all, write positions 2..kArmsU+1 */
+    const int last = e.cnt - 1;
+    double xs[kArmsU + 2], ys[kArmsU + 2];
+#pragma unroll
+    for (int k = 0; k < kArmsU + 2; k++) {
+      xs[k] = e.X(k);
+      ys[k] = e.Y(k);
+    }
+#pragma unroll
+    for (int k = 0; k < kArmsU; k++) {
+      const bool mv = (k >= pr && k <= last);
+      e.sX(k + 2, mv ? xs[k] : xs[k + 2]);
+      e.sY(k + 2, mv ? ys[k] : ys[k + 2]);
+    }
+  } else {
+    for (int k = e.cnt - 1; k >= pr; k--) {
+      e.sX(k + 2, e.X(k));
+      e.sY(k + 2, e.Y(k));
+    }
   }
   e.cnt += 2;
   const int qi = ((pr - 1) & 1) ? pr + 1 : pr;
@@ -326,6 +404,61 @@ __device__ __forceinline__ int arms_loop(Env &e, F &f, double xprev, double ypre
     xsamp = (um > w) ? xprev : p.x;
     return 0;
   }
+}
+
+/* Metropolis step that ends an accepted iteration (src/arms.c:190-213) */
+template <class Env>
+__device__ __forceinline__ double arms_metropolis(const Env &e, const WPt &p, double ynew, double xprev, double yprev,
+                                                  Lane &ln) {
+  int ql = 0;
+  while (e.X(ql + 1) < xprev) ql++;
+  const int qr = ql + 1;
+  const double xql = e.X(ql), yql = e.Y(ql);
+  double w = PHT_DIV((xprev - xql), (e.X(qr) - xql));
+  double zold = yql + w * (e.Y(qr) - yql);
+  double znew = p.y;
+  if (yprev < zold) zold = yprev;
+  if (ynew < znew) znew = ynew;
+  w = ynew - znew - yprev + zold;
+  if (w > 0.0) w = 0.0;
+  w = (w > -kYCeil) ? pht_exp_core(w) : 0.0;
+  const double um = dev_u(ln.r);
+  return (um > w) ? xprev : p.x;
+}
+
+/* Step-wise arms_loop for persistent kernels: a lane whose proposal was
+ * rejected keeps the rejected point pending and performs ONE step per call
+ * (the envelope update that ends the rejected iteration, then the next
+ * iteration), so a wavefront never waits for its longest rejection chain.
+ * Draws, evaluations and results are those of arms_loop. */
+struct ArmsPend {
+  double px, py, pey, yprev;
+  int pr, it; /* it: index of the next iteration */
+};
+
+/* returns 0 (xsamp set), 1 (still pending) or 4 (iteration cap) */
+template <class Env, class F>
+__device__ __forceinline__ int arms_step(Env &e, F &f, ArmsPend &pd, double xprev, double &xsamp, Lane &ln) {
+  WPt p;
+  p.x = pd.px; p.y = pd.py; p.ey = pd.pey; p.pr = pd.pr;
+  arms_update(e, p, f, ln);
+  if (pd.it >= kArmsMaxIt) {
+    xsamp = xprev;
+    return 4;
+  }
+  WPt q;
+  arms_invert(e, dev_u(ln.r), q);
+  const double u = dev_u(ln.r) * q.ey;
+  const double y = logshift(u, e.ymax);
+  const double ynew = f(q.x);
+  ln.neval++;
+  if (y >= ynew) {
+    pd.px = q.x; pd.py = ynew; pd.pey = expshift(ynew, e.ymax); pd.pr = q.pr;
+    pd.it++;
+    return 1;
+  }
+  xsamp = arms_metropolis(e, q, ynew, xprev, pd.yprev, ln);
+  return 0;
 }
 
 /* arms() as used by the reference (xprev 0, one sample).  Returns 0, an
@@ -483,7 +616,7 @@ __device__ __forceinline__ void env9_invert(const Env9 &e, double prob, WPt &p) 
  * used only after a rejection.  Same draws, evaluations and results. */
 template <class Env, class F>
 __device__ __forceinline__ int arms_fast(Env &slow, const double xinit[4], double xl, double xr, F &f, double xprev,
-                                         double &xsamp, Lane &ln) {
+                                         double &xsamp, Lane &ln, ArmsPend *pend = nullptr) {
   if ((xinit[0] <= xl) || (xinit[3] >= xr)) return 1003;
   if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) return 1004;
   Env9 e;
@@ -515,6 +648,7 @@ __device__ __forceinline__ int arms_fast(Env &slow, const double xinit[4], doubl
   const double yv = logshift(u, e.ymax);
   const double ynew = f(p.x);
   ln.neval++;
+  PHT_STAMP(ln, 5);
   if (yv >= ynew) {
     /* rejected: hand the envelope to the general code */
     slow.cnt = 9;
@@ -527,8 +661,16 @@ __device__ __forceinline__ int arms_fast(Env &slow, const double xinit[4], doubl
     slow.ymax = e.ymax;
     p.y = ynew;
     p.ey = expshift(p.y, e.ymax);
+    if (pend) { /* the caller continues with arms_step() */
+      pend->px = p.x; pend->py = p.y; pend->pey = p.ey; pend->pr = p.pr;
+      pend->yprev = yprev;
+      pend->it = 1;
+      return -1;
+    }
     arms_update(slow, p, f, ln);
-    return arms_loop(slow, f, xprev, yprev, xsamp, ln, 1);
+    const int rc = arms_loop(slow, f, xprev, yprev, xsamp, ln, 1);
+    PHT_STAMP(ln, 4);
+    return rc;
   }
   /* Metropolis step: ql = first k with x[k+1] >= xprev */
   int ql = 0;
@@ -663,32 +805,14 @@ __device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink 
   return fin;
 }
 
-/* one non-absorbing jump: ARMS sojourn (:307-342), moveMass + categorical
- * (:350-358), statistics (:362-363) */
-template <int NT, class Env, class Sink>
-__device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st) {
+/* end of a non-absorbing jump once the sojourn d is drawn: moveMass +
+ * categorical (:350-358), statistics (:362-363) */
+template <int NT, class Sink>
+__device__ __forceinline__ void ecs_jump_finish(const Par<NT> &P, Lane &ln, Sink &sk, EcsLane<NT> &st,
+                                                const EcsDens<NT> &f, double xsamp, int ainfo) {
   const int n = P.n();
   const int j = st.j;
   const double y_t = st.yt;
-  const double Sjj = P.S(j, j);
-  if (!st.haveE0) { /* s_j = 0: no absorb test ran at this state */
-#pragma unroll
-    for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
-    st.haveE0 = true;
-  }
-  EcsDens<NT> f{P, j, y_t, Sjj, st.E0, true, -1.0, {}};
-  double xinit[4];
-  xinit[0] = (y_t) / 1e6;
-  xinit[1] = (y_t) / 3.0;
-  xinit[2] = xinit[1] * 2.0;
-  xinit[3] = y_t - xinit[0];
-  double xsamp = 0.0;
-#ifdef PHT_ECS_NOFAST
-  const int ainfo = arms(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln);
-#else
-  const int ainfo = arms_fast(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln);
-#endif
-  PHT_STAMP(ln, 2);
   if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
   const double d = xsamp;
   const double x = y_t - d;
@@ -745,6 +869,61 @@ __device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, S
   st.njump++;
   st.j = nj;
   PHT_STAMP(ln, 3);
+}
+
+template <int NT>
+__device__ __forceinline__ EcsDens<NT> ecs_dens(const Par<NT> &P, EcsLane<NT> &st) {
+  return EcsDens<NT>{P, st.j, st.yt, P.S(st.j, st.j), st.E0, true, -1.0, {}};
+}
+
+/* start of a non-absorbing jump: ARMS sojourn (:307-342).  With `pend`
+ * non-null a rejected first proposal leaves the jump pending (false is
+ * returned; continue with ecs_jump_resume); otherwise the jump completes. */
+template <int NT, class Env, class Sink>
+__device__ __forceinline__ bool ecs_jump_start(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st,
+                                               ArmsPend *pend) {
+  const int n = P.n();
+  const double y_t = st.yt;
+  if (!st.haveE0) { /* s_j = 0: no absorb test ran at this state */
+#pragma unroll
+    for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
+    st.haveE0 = true;
+  }
+  EcsDens<NT> f = ecs_dens(P, st);
+  double xinit[4];
+  xinit[0] = (y_t) / 1e6;
+  xinit[1] = (y_t) / 3.0;
+  xinit[2] = xinit[1] * 2.0;
+  xinit[3] = y_t - xinit[0];
+  double xsamp = 0.0;
+#ifdef PHT_ECS_NOFAST
+  (void)pend;
+  const int ainfo = arms(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln);
+#else
+  const int ainfo = arms_fast(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln, pend);
+  if (ainfo == -1) return false;
+#endif
+  PHT_STAMP(ln, 2);
+  ecs_jump_finish(P, ln, sk, st, f, xsamp, ainfo);
+  return true;
+}
+
+/* one ARMS step of a pending jump; true when the jump completed */
+template <int NT, class Env, class Sink>
+__device__ __forceinline__ bool ecs_jump_resume(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st,
+                                                ArmsPend &pend) {
+  EcsDens<NT> f = ecs_dens(P, st);
+  double xsamp = 0.0;
+  const int rc = arms_step(env, f, pend, 0.0, xsamp, ln);
+  if (rc == 1) return false;
+  ecs_jump_finish(P, ln, sk, st, f, xsamp, rc);
+  return true;
+}
+
+/* one complete non-absorbing jump */
+template <int NT, class Env, class Sink>
+__device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st) {
+  ecs_jump_start(P, ln, env, sk, st, nullptr);
 }
 
 template <int NT, class Env, class Sink>

@@ -1,0 +1,343 @@
+/*
+ * pht_ecs_round.h — the ARMS part of one round of the persistent ECS-exact
+ * kernel, converged across lanes.
+ *
+ * In a round every lane that needs a sojourn is either
+ *   starting  a jump: fresh 9-point envelope (4 density evaluations), or
+ *   pending : its previous proposal was rejected; the envelope update that
+ *             ends that iteration (src/arms.c:525-621) is due, then the
+ *             next iteration.
+ * Both kinds then run the SAME code: meets, cumulate, invert, one density
+ * evaluation, the acceptance test, Metropolis and moveMass.  The envelope
+ * lives in EnvLds with compile-time positions 0..kRoundCap-1 (predicated by
+ * the lane's cnt), so these blocks execute once per round for all jumping
+ * lanes instead of once per lane kind and rejection chain.  Lanes whose
+ * envelope would outgrow kRoundCap use the general code (arms_step).
+ *
+ * Same draws, same evaluations, same arithmetic per lane as arms() /
+ * arms_loop(): meet() is a pure function of its neighbours (and of cnt
+ * through the boundary flags), so recomputing every intersection point
+ * after an update reproduces the reference's targeted recomputation of the
+ * ones next to the new point (src/arms.c:600-615) value for value.
+ */
+#ifndef PHT_ECS_ROUND_H
+#define PHT_ECS_ROUND_H
+
+#include "pht_device.h"
+
+namespace pht {
+
+constexpr int kRoundCap = 13; /* envelope points handled by the converged code */
+
+/* meet() at compile-time position K of an envelope with `last` = cnt - 1;
+ * positions beyond last are left as they are.  Branch-free form of
+ * arms_meet (same expressions, selected). */
+template <int K, int CAP, class Env>
+__device__ __forceinline__ void round_meet(Env &e, int last) {
+  /* last <= CAP - 1: neighbours at or beyond CAP are never used */
+  const bool active = (K <= last);
+  const bool il = (K >= 3), ir = (K + 3 <= last), irl = (K >= 1 && K + 1 <= last);
+  const double xk = e.X(K), yk = e.Y(K);
+  double xm1 = 0.0, ym1 = 0.0, xm3 = 0.0, ym3 = 0.0, xp1 = 0.0, yp1 = 0.0, xp3 = 0.0, yp3 = 0.0;
+  if constexpr (K >= 1) { xm1 = e.X(K - 1); ym1 = e.Y(K - 1); }
+  if constexpr (K >= 3) { xm3 = e.X(K - 3); ym3 = e.Y(K - 3); }
+  if constexpr (K + 1 < CAP) { xp1 = e.X(K + 1); yp1 = e.Y(K + 1); }
+  if constexpr (K + 3 < CAP) { xp3 = e.X(K + 3); yp3 = e.Y(K + 3); }
+  double gl = 0.0, gr = 0.0, grl = 0.0, dl = 0.0, dr = 0.0;
+  if constexpr (K >= 3) gl = PHT_DIV((ym1 - ym3), (xm1 - xm3));
+  gr = ir ? PHT_DIV((yp1 - yp3), (xp1 - xp3)) : 0.0;
+  grl = irl ? PHT_DIV((yp1 - ym1), (xp1 - xm1)) : 0.0;
+  if (irl && il && (gl < grl)) gl = gl + (1.0 + 1.0) * (grl - gl);
+  if (irl && ir && (gr > grl)) gr = gr + (1.0 + 1.0) * (grl - gr);
+  if (il && irl) {
+    dr = (gl - grl) * (xp1 - xm1);
+    dr = (dr < kYEps) ? kYEps : dr;
+  }
+  if (ir && irl) {
+    dl = (grl - gr) * (xp1 - xm1);
+    dl = (dl < kYEps) ? kYEps : dl;
+  }
+  double nx = xk, ny = yk;
+  if (il && ir && irl) {
+    nx = PHT_DIV((dl * xp1 + dr * xm1), (dl + dr));
+    ny = PHT_DIV((dl * yp1 + dr * ym1 + dl * dr), (dl + dr));
+  } else if (il && irl) {
+    nx = xp1;
+    ny = yp1 + dr;
+  } else if (ir && irl) {
+    nx = xm1;
+    ny = ym1 + dl;
+  } else if (il) {
+    ny = ym1 + gl * (xk - xm1);
+  } else if (ir) {
+    ny = yp1 - gr * (xp1 - xk);
+  }
+  if (active) {
+    e.sX(K, nx);
+    e.sY(K, ny);
+  }
+}
+
+template <int CAP, class Env>
+__device__ __forceinline__ void round_meets(Env &e, int last) {
+  round_meet<0, CAP>(e, last);
+  round_meet<2, CAP>(e, last);
+  round_meet<4, CAP>(e, last);
+  round_meet<6, CAP>(e, last);
+  round_meet<8, CAP>(e, last);
+  if constexpr (CAP > 9) round_meet<10, CAP>(e, last);
+  if constexpr (CAP > 11) round_meet<12, CAP>(e, last);
+}
+
+/* arms_cumulate over the first CAP positions (cnt <= CAP) */
+template <int CAP, class Env>
+__device__ __forceinline__ void round_cumulate(Env &e) {
+  const int cnt = e.cnt;
+  double xs[CAP], ys[CAP];
+#pragma unroll
+  for (int k = 0; k < CAP; k++) {
+    xs[k] = e.X(k);
+    ys[k] = e.Y(k);
+  }
+  double ymax = ys[0];
+#pragma unroll
+  for (int k = 1; k < CAP; k++) ymax = (k < cnt && ys[k] > ymax) ? ys[k] : ymax;
+  e.ymax = ymax;
+  double eyp = expshift(ys[0], ymax);
+  double cum = 0.;
+  e.sCUM(0, cum);
+#pragma unroll
+  for (int k = 1; k < CAP; k++) {
+    const double xp = xs[k - 1], xk = xs[k], yp = ys[k - 1], yk = ys[k];
+    const double eyk = expshift(yk, ymax);
+    const double lin = 0.5 * (eyk + eyp) * (xk - xp);
+    const double ex = (PHT_DIV((eyk - eyp), (yk - yp))) * (xk - xp);
+    const double a = (xp == xk) ? 0. : ((fabs(yk - yp) < kYEps) ? lin : ex);
+    cum = cum + a;
+    e.sCUM(k, cum);
+    eyp = eyk;
+  }
+}
+
+/* arms_invert with the unrolled scan; ey of the two segment ends recomputed */
+template <int CAP, class Env>
+__device__ __forceinline__ void round_invert(Env &e, double prob, WPt &p) {
+  const int last = e.cnt - 1;
+  double cs[CAP];
+#pragma unroll
+  for (int k = 0; k < CAP; k++) cs[k] = e.CUM(k);
+  const double u = prob * e.CUM(last);
+  int q = last;
+  bool go = true;
+#pragma unroll
+  for (int k = CAP - 2; k >= 1; k--) {
+    if (k <= last - 1) {
+      go = go && (cs[k] > u);
+      q = go ? k : q;
+    }
+  }
+  p.pr = q;
+  const double cr = e.CUM(q), cl = e.CUM(q - 1);
+  const double prop = PHT_DIV((u - cl), (cr - cl));
+  const double xl = e.X(q - 1), xr = e.X(q);
+  const double yr = e.Y(q), yl = e.Y(q - 1);
+  const double eyr = expshift(yr, e.ymax);
+  if (xl == xr) {
+    p.x = xr; p.y = yr; p.ey = eyr;
+    return;
+  }
+  const double eyl = expshift(yl, e.ymax);
+  if (fabs(yr - yl) < kYEps) {
+    if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
+      p.x = xl + (PHT_DIV((xr - xl), (eyr - eyl))) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
+    else
+      p.x = xl + (xr - xl) * prop;
+    p.ey = (PHT_DIV((p.x - xl), (xr - xl))) * (eyr - eyl) + eyl;
+    p.y = logshift(p.ey, e.ymax);
+  } else {
+    p.x = xl + (PHT_DIV((xr - xl), (yr - yl))) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
+    p.y = (PHT_DIV((p.x - xl), (xr - xl))) * (yr - yl) + yl;
+    p.ey = expshift(p.y, e.ymax);
+  }
+}
+
+/* the first half of arms_update (shift + insert + XEPS adjustment), for an
+ * envelope that stays within kRoundCap points; meets and cumulate follow
+ * in the converged block */
+template <int CAP, class Env, class F>
+__device__ __forceinline__ void round_insert(Env &e, const ArmsPend &pd, F &f, Lane &ln) {
+  /* cnt + 2 <= CAP */
+  const int pr = pd.pr;
+  const int last = e.cnt - 1;
+  double xs[CAP], ys[CAP];
+#pragma unroll
+  for (int k = 0; k < CAP; k++) {
+    xs[k] = e.X(k);
+    ys[k] = e.Y(k);
+  }
+#pragma unroll
+  for (int k = 0; k + 2 < CAP; k++) {
+    const bool mv = (k >= pr && k <= last);
+    e.sX(k + 2, mv ? xs[k] : xs[k + 2]);
+    e.sY(k + 2, mv ? ys[k] : ys[k + 2]);
+  }
+  e.cnt += 2;
+  const int qi = ((pr - 1) & 1) ? pr + 1 : pr;
+  e.sX(qi, pd.px);
+  e.sY(qi, pd.py);
+  const int ql = (qi >= 2) ? qi - 2 : qi - 1;
+  const int qr = (qi + 2 <= e.cnt - 1) ? qi + 2 : qi + 1;
+  const double xl = e.X(ql), xr = e.X(qr);
+  if (pd.px < (1. - kXEps) * xl + kXEps * xr) {
+    const double xn = (1. - kXEps) * xl + kXEps * xr;
+    e.sX(qi, xn);
+    e.sY(qi, f(xn));
+    ln.neval++;
+  } else if (pd.px > kXEps * xl + (1. - kXEps) * xr) {
+    const double xn = kXEps * xl + (1. - kXEps) * xr;
+    e.sX(qi, xn);
+    e.sY(qi, f(xn));
+    ln.neval++;
+  }
+}
+
+/* Metropolis step with the scan unrolled over the converged envelope */
+template <class Env>
+__device__ __forceinline__ double round_metropolis(const Env &e, const WPt &p, double ynew, double xprev, double yprev,
+                                                   Lane &ln) {
+  int ql = 0;
+  while (e.X(ql + 1) < xprev) ql++;
+  const int qr = ql + 1;
+  const double xql = e.X(ql), yql = e.Y(ql);
+  double w = PHT_DIV((xprev - xql), (e.X(qr) - xql));
+  double zold = yql + w * (e.Y(qr) - yql);
+  double znew = p.y;
+  if (yprev < zold) zold = yprev;
+  if (ynew < znew) znew = ynew;
+  w = ynew - znew - yprev + zold;
+  if (w > 0.0) w = 0.0;
+  w = (w > -kYCeil) ? pht_exp_core(w) : 0.0;
+  const double um = dev_u(ln.r);
+  return (um > w) ? xprev : p.x;
+}
+
+/*
+ * One converged ARMS round for the lanes with `start` (begin a jump at
+ * st.j) or `pend` (continue one).  On return pend tells whether the lane's
+ * jump is still pending; completed jumps have been recorded (moveMass,
+ * statistics) exactly as ecs_jump_finish does.
+ */
+template <int NT, class Env, class Sink>
+__device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st, bool start,
+                                          bool &pend, ArmsPend &pd) {
+  const int n = P.n();
+  const double y_t = st.yt;
+  if (start && !st.haveE0) { /* s_j = 0: no absorb test ran at this state */
+#pragma unroll
+    for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
+    st.haveE0 = true;
+  }
+  EcsDens<NT> f = ecs_dens(P, st);
+  double xsamp = 0.0;
+  int ainfo = 0;
+  bool fin = false;  /* the jump ends this round without an iteration */
+  bool big = false;  /* envelope outgrows kRoundCap: general code */
+
+  /* ---- starting lanes: initial envelope (arms(), src/arms.c:226-333) */
+  if (start) {
+    double xinit[4];
+    xinit[0] = (y_t) / 1e6;
+    xinit[1] = (y_t) / 3.0;
+    xinit[2] = xinit[1] * 2.0;
+    xinit[3] = y_t - xinit[0];
+    if ((xinit[0] <= 0.0) || (xinit[3] >= y_t)) {
+      ainfo = 1003;
+      fin = true;
+    } else if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) {
+      ainfo = 1004;
+      fin = true;
+    } else {
+      env.cnt = 9;
+      env.sX(0, 0.0);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        env.sX(2 * k + 1, xinit[k]);
+        env.sY(2 * k + 1, f(xinit[k]));
+      }
+      ln.neval += 4;
+      env.sX(8, y_t);
+    }
+  }
+  /* ---- pending lanes: the update that ends the rejected iteration */
+  if (pend) big = (env.cnt + 2 > kRoundCap);
+  if (__any(pend && !big && env.cnt > 9)) {
+    if (pend && !big) round_insert<13>(env, pd, f, ln);
+  } else {
+    if (pend && !big) round_insert<11>(env, pd, f, ln);
+  }
+  PHT_STAMP(ln, 1);
+  /* ---- converged: intersections and areas over the widest envelope in
+   * the wavefront (9, 11 or 13 points) */
+  const bool arm = (start && !fin) || (pend && !big);
+  const int cap = __any(arm && env.cnt > 11) ? 13 : (__any(arm && env.cnt > 9) ? 11 : 9);
+  if (arm) {
+    if (cap == 9) {
+      round_meets<9>(env, env.cnt - 1);
+      round_cumulate<9>(env);
+    } else if (cap == 11) {
+      round_meets<11>(env, env.cnt - 1);
+      round_cumulate<11>(env);
+    } else {
+      round_meets<13>(env, env.cnt - 1);
+      round_cumulate<13>(env);
+    }
+  }
+  if (start && !fin) {
+    pd.yprev = f(0.0); /* xprev = 0 lies in [xl, xr] = [0, y_t] */
+    ln.neval++;
+    pd.it = 0;
+  }
+  /* the iteration cap is checked after the update (arms_loop) */
+  if (pend && !big && pd.it >= kArmsMaxIt) {
+    ainfo = 4;
+    fin = true;
+  }
+  PHT_STAMP(ln, 5);
+  /* ---- converged: one iteration (sample, evaluate, test) */
+  bool acc = false;
+  if (arm && !fin) {
+    WPt q;
+    const double pu = dev_u(ln.r);
+    if (cap == 9) round_invert<9>(env, pu, q);
+    else if (cap == 11) round_invert<11>(env, pu, q);
+    else round_invert<13>(env, pu, q);
+    const double u = dev_u(ln.r) * q.ey;
+    const double yv = logshift(u, env.ymax);
+    const double ynew = f(q.x);
+    ln.neval++;
+    if (yv >= ynew) {
+      pd.px = q.x; pd.py = ynew; pd.pey = expshift(ynew, env.ymax); pd.pr = q.pr;
+      pd.it++;
+      pend = true;
+    } else {
+      xsamp = round_metropolis(env, q, ynew, 0.0, pd.yprev, ln);
+      acc = true;
+    }
+  }
+  /* ---- rare: envelopes beyond kRoundCap continue in the general code */
+  if (big) {
+    const int rc = arms_step(env, f, pd, 0.0, xsamp, ln);
+    if (rc != 1) {
+      ainfo = rc;
+      acc = true;
+    }
+  }
+  PHT_STAMP(ln, 2);
+  if (acc || fin) {
+    pend = false;
+    ecs_jump_finish(P, ln, sk, st, f, xsamp, ainfo);
+  }
+}
+
+}  // namespace pht
+#endif

@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include "pht_device.h"
+#include "pht_ecs_round.h"
 #include "pht_env.h"
 #include "pht_kernels.h"
 
@@ -157,6 +158,9 @@ static int smem_bytes(int n) {
 #define PHT_ENV_K 11
 #endif
 constexpr int kEnvK = PHT_ENV_K;
+#ifndef PHT_SLOW_K
+#define PHT_SLOW_K 10
+#endif
 
 #ifndef PHT_ECS_WAVES
 #define PHT_ECS_WAVES 0
@@ -197,9 +201,13 @@ ecs_exact_kernel(SweepArgs a) {
   EnvLds<kEnvK, kBlock> env;
   double spill[3 * EnvLds<kEnvK, kBlock>::kSpill];
   env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill);
+#elif PHT_SLOW_K > 0
+  /* fresh envelopes live in registers (arms_fast); updated ones (after a
+   * rejection) in LDS, lane-interleaved, points >= PHT_SLOW_K in scratch */
+  EnvLds<PHT_SLOW_K, kBlock> env;
+  double spill[3 * EnvLds<PHT_SLOW_K, kBlock>::kSpill];
+  env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill);
 #else
-  /* fresh envelopes live in registers (arms_fast); this one only takes the
-   * rarely updated ones */
   (void)envl;
   EnvPrivate env;
 #endif
@@ -225,9 +233,13 @@ ecs_exact_kernel(SweepArgs a) {
     ny = a.y[a.begin + nextp];
     ngid = a.gid[a.begin + nextp];
   }
+  /* a lane whose sojourn proposal was rejected finishes that jump one ARMS
+   * step per round (ecs_jump_resume) while the other lanes go on */
+  ArmsPend pd;
+  bool pend = false;
   for (;;) {
     bool need = false;
-    while (!done) {
+    while (!done && !pend) {
       if (!have) {
         if (nextp >= a.count) {
           done = true;
@@ -270,12 +282,20 @@ ecs_exact_kernel(SweepArgs a) {
       break;
     }
     PHT_STAMP(ln, 0);
-    if (!__any(need)) break;
+    if (!__any(need) && !__any(pend)) break;
+#if defined(PHT_ECS_NOFAST)
     if (need) ecs_jump(P, ln, env, sk, st);
+#elif defined(PHT_ECS_PEND)
+    if (pend) pend = !ecs_jump_resume(P, ln, env, sk, st, pd);
+    PHT_STAMP(ln, 4);
+    if (need) pend = !ecs_jump_start(P, ln, env, sk, st, &pd);
+#else
+    ecs_round(P, ln, env, sk, st, need, pend, pd);
+#endif
   }
 #ifdef PHT_STAMPS
   if ((threadIdx.x & 63) == 0)
-    for (int q = 0; q < 4; q++) lds_add(&xc[8 + q], ln.st_acc[q]);
+    for (int q = 0; q < 8; q++) lds_add(&xc[8 + q], ln.st_acc[q]);
 #endif
   __syncthreads();
   unsigned long long *g = a.stats;
@@ -293,7 +313,7 @@ static int smem_bytes_ecs(int n) {
 #ifdef PHT_ECS_NOFAST
   return ((smem_bytes(n) + 4 + 15) & ~15) + EnvLds<kEnvK, kBlock>::lds_doubles_per_lane() * 8 * kBlock;
 #else
-  return (smem_bytes(n) + 4 + 15) & ~15;
+  return ((smem_bytes(n) + 4 + 15) & ~15) + 3 * PHT_SLOW_K * 8 * kBlock;
 #endif
 }
 
