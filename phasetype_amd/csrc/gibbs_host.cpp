@@ -419,9 +419,8 @@ extern "C" void pht_ctx_destroy(pht_ctx *c) {
 /*
  * Upload this shard's observations.  obs0 = global index of y[0]; the
  * Philox counter of observation i is obs0 + i whatever the shard layout.
- * Observations are reordered on the device (exact before censored, then by
- * y) so a wavefront's lanes carry similar path lengths; results do not
- * depend on the order.
+ * Observations are reordered on the device (exact before censored, see
+ * below); results do not depend on the order.
  */
 extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, long count, long obs0) {
   HIPCHK(hipSetDevice(c->device));
@@ -431,10 +430,17 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
   if (count == 0) return 0;
   std::vector<long> ord(count);
   std::iota(ord.begin(), ord.end(), 0L);
+  /* exact observations by decreasing y: the persistent kernel hands out
+   * long paths first and ends on short ones (a short tail); censored ones
+   * (one lane per observation) by increasing y.  PHT_ORDER=asc|none: A/B. */
+  const char *oe = getenv("PHT_ORDER");
+  const int omode = !oe ? 0 : (!strcmp(oe, "asc") ? 1 : (!strcmp(oe, "none") ? 2 : 0));
   std::stable_sort(ord.begin(), ord.end(), [&](long a, long b) {
     const int ca = cens[a] != 0, cb = cens[b] != 0;
     if (ca != cb) return ca < cb;
-    return y[a] < y[b];
+    if (ca) return y[a] < y[b];
+    if (omode == 2) return false;
+    return omode == 1 ? (y[a] < y[b]) : (y[a] > y[b]);
   });
   std::vector<double> ys(count);
   std::vector<int> cs(count);
