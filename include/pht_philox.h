@@ -8,13 +8,16 @@
  *   key     = (k0, k1)                  — two words from R's stream at
  *                                         LJMA_Gibbs entry (gibbs_host.cpp)
  *   counter = (obs, stream, sweep, blk) — obs index, stream tag (0 = main),
- *                                         Gibbs sweep, 64-bit-pair block
- * One Philox block yields two uniforms (words 0,1 then 2,3).  Uniform draw
- * number i of an observation comes from block i/2, half i%2, so any lane can
- * replay any observation from any draw index (used by the MHRS kernel).
+ *                                         Gibbs sweep, block index
+ * An observation's stream is the word sequence block 0 words 0..3, block 1
+ * words 0..3, ...; word number i comes from block i/4, so any lane can
+ * replay any observation from any word index (used by the MHRS kernel).
  *
- * uniform: m = (w_hi << 20) | (w_lo >> 12) (52 bits), u = (2m+1) * 2^-53,
- * so u is exact and 0 < u < 1.
+ * uniform  (one word w):    u = (2w+1) * 2^-33, exact, 0 < u < 1 — the
+ *                           resolution of R's unif_rand (2^-32);
+ * uniform53 (two words a,b): m = (a << 20) | (b >> 12) (52 bits),
+ *                           u = (2m+1) * 2^-53 — used where the tail of
+ *                           -log(u) matters (exponential sojourns).
  */
 #ifndef PHT_PHILOX_H
 #define PHT_PHILOX_H
@@ -57,38 +60,80 @@ PHT_HD2 double pht_u01(uint32_t whi, uint32_t wlo) {
   return (double)(2 * m + 1) * 1.1102230246251565404e-16; /* 2^-53 */
 }
 
-/* Per-observation uniform stream with a one-uniform buffer. */
+/* Per-observation word stream.  The current block is a shift register
+ * (a0 is the next word, na words left); a second block (b0..b3, valid when
+ * nb) can be generated ahead at a convenient point (pht_stream_topup): on a
+ * GPU, at a point where a whole wavefront executes it once, instead of at
+ * whichever draw finds the buffer empty.  The word sequence is the same
+ * whenever blocks are generated. */
 typedef struct {
   uint32_t k0, k1;     /* key */
   uint32_t obs, tag;   /* counter words 0,1 */
   uint32_t sweep;      /* counter word 2 */
-  uint32_t blk;        /* counter word 3: next Philox block */
-  double buf;          /* second uniform of the last block */
-  int have;            /* buf valid */
+  uint32_t blk;        /* counter word 3: next block to generate */
+  uint32_t a0, a1, a2, a3;
+  uint32_t b0, b1, b2, b3;
+  int na, nb;
 } pht_stream;
 
 PHT_HD2 void pht_stream_init(pht_stream *s, uint32_t k0, uint32_t k1, uint32_t obs,
                              uint32_t tag, uint32_t sweep) {
   s->k0 = k0; s->k1 = k1; s->obs = obs; s->tag = tag; s->sweep = sweep;
-  s->blk = 0; s->buf = 0.0; s->have = 0;
+  s->blk = 0; s->na = 0; s->nb = 0;
+  s->a0 = s->a1 = s->a2 = s->a3 = 0u;
+  s->b0 = s->b1 = s->b2 = s->b3 = 0u;
 }
 
-/* number of uniforms drawn so far */
-PHT_HD2 uint32_t pht_stream_pos(const pht_stream *s) { return 2 * s->blk - (uint32_t)s->have; }
+PHT_HD2 pht_u32x4 pht_stream_block(pht_stream *s) {
+  pht_u32x4 c; c.v[0] = s->obs; c.v[1] = s->tag; c.v[2] = s->sweep; c.v[3] = s->blk++;
+  return pht_philox4x32_10(c, s->k0, s->k1);
+}
+
+/* generate the next block ahead (no effect on the word sequence) */
+PHT_HD2 void pht_stream_topup(pht_stream *s) {
+  if (!s->nb) {
+    pht_u32x4 w = pht_stream_block(s);
+    s->b0 = w.v[0]; s->b1 = w.v[1]; s->b2 = w.v[2]; s->b3 = w.v[3];
+    s->nb = 1;
+  }
+}
+
+PHT_HD2 uint32_t pht_next_w(pht_stream *s) {
+  if (s->na == 0) {
+    if (s->nb) {
+      s->a0 = s->b0; s->a1 = s->b1; s->a2 = s->b2; s->a3 = s->b3;
+      s->nb = 0;
+    } else {
+      pht_u32x4 w = pht_stream_block(s);
+      s->a0 = w.v[0]; s->a1 = w.v[1]; s->a2 = w.v[2]; s->a3 = w.v[3];
+    }
+    s->na = 4;
+  }
+  const uint32_t w = s->a0;
+  s->a0 = s->a1; s->a1 = s->a2; s->a2 = s->a3;
+  s->na--;
+  return w;
+}
+
+/* number of words drawn so far */
+PHT_HD2 uint32_t pht_stream_pos(const pht_stream *s) {
+  return 4u * s->blk - (uint32_t)s->na - 4u * (uint32_t)s->nb;
+}
 
 PHT_HD2 double pht_next_u(pht_stream *s) {
-  if (s->have) { s->have = 0; return s->buf; }
-  pht_u32x4 c; c.v[0] = s->obs; c.v[1] = s->tag; c.v[2] = s->sweep; c.v[3] = s->blk++;
-  pht_u32x4 w = pht_philox4x32_10(c, s->k0, s->k1);
-  s->buf = pht_u01(w.v[2], w.v[3]);
-  s->have = 1;
-  return pht_u01(w.v[0], w.v[1]);
+  return (double)(2.0 * (double)pht_next_w(s) + 1.0) * 1.16415321826934814453125e-10; /* 2^-33 */
 }
 
-/* reposition to uniform index pos (replay) */
+PHT_HD2 double pht_next_u53(pht_stream *s) {
+  const uint32_t a = pht_next_w(s);
+  const uint32_t b = pht_next_w(s);
+  return pht_u01(a, b);
+}
+
+/* reposition to word index pos (replay) */
 PHT_HD2 void pht_stream_seek(pht_stream *s, uint32_t pos) {
-  s->blk = pos >> 1; s->have = 0;
-  if (pos & 1u) (void)pht_next_u(s);
+  s->blk = pos >> 2; s->na = 0; s->nb = 0;
+  for (uint32_t i = 0; i < (pos & 3u); i++) (void)pht_next_w(s);
 }
 
 #endif /* PHT_PHILOX_H */

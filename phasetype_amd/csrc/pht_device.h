@@ -109,7 +109,7 @@ __device__ __forceinline__ double dev_runif(pht_stream &r, double a, double b) {
 }
 __device__ __forceinline__ double dev_rexp(pht_stream &r, double scale) {
   if (!isfinite(scale) || scale <= 0.0) return scale == 0.0 ? 0.0 : __builtin_nan("");
-  return scale * -pht_log(pht_next_u(&r));
+  return scale * -pht_log(pht_next_u53(&r));
 }
 
 /* Lane context: random stream, flags and counters of the current observation. */
@@ -120,7 +120,7 @@ struct Lane {
   int nbrent;
   int njump;
 #ifdef PHT_STAMPS
-  unsigned long long st_last, st_acc[8];
+  unsigned long long st_last, st_acc[8], st_rounds;
 #endif
 };
 
@@ -868,7 +868,6 @@ __device__ __forceinline__ void ecs_jump_finish(const Par<NT> &P, Lane &ln, Sink
   ln.njump++;
   st.njump++;
   st.j = nj;
-  PHT_STAMP(ln, 3);
 }
 
 template <int NT>
@@ -1122,7 +1121,7 @@ __device__ __forceinline__ void bladt_replay(const Par<NT> &P, double y, int cen
       const double sc = 1.0 / -P.S(j, j);
       double e;
       if (!isfinite(sc) || sc <= 0.0) e = (sc == 0.0) ? 0.0 : __builtin_nan("");
-      else e = sc * -pht_log(pht_next_u(&r));
+      else e = sc * -pht_log(pht_next_u53(&r));
       t = t + e;
     }
     target = pht_next_u(&r);

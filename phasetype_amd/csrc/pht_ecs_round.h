@@ -232,6 +232,9 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
                                           bool &pend, ArmsPend &pd) {
   const int n = P.n();
   const double y_t = st.yt;
+  /* converged: the next Philox block for this round's draws (invert, test,
+   * Metropolis, moveMass: at most 4 words) */
+  if (start || pend) pht_stream_topup(&ln.r);
   if (start && !st.haveE0) { /* s_j = 0: no absorb test ran at this state */
 #pragma unroll
     for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
@@ -292,6 +295,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
       round_cumulate<13>(env);
     }
   }
+  PHT_STAMP(ln, 4);
   if (start && !fin) {
     pd.yprev = f(0.0); /* xprev = 0 lies in [xl, xr] = [0, y_t] */
     ln.neval++;
@@ -305,16 +309,24 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
   PHT_STAMP(ln, 5);
   /* ---- converged: one iteration (sample, evaluate, test) */
   bool acc = false;
-  if (arm && !fin) {
-    WPt q;
+  const bool itr = arm && !fin;
+  WPt q;
+  double yv = 0.0, ynew = 0.0;
+  if (itr) {
     const double pu = dev_u(ln.r);
     if (cap == 9) round_invert<9>(env, pu, q);
     else if (cap == 11) round_invert<11>(env, pu, q);
     else round_invert<13>(env, pu, q);
     const double u = dev_u(ln.r) * q.ey;
-    const double yv = logshift(u, env.ymax);
-    const double ynew = f(q.x);
+    yv = logshift(u, env.ymax);
+  }
+  PHT_STAMP(ln, 6);
+  if (itr) {
+    ynew = f(q.x);
     ln.neval++;
+  }
+  PHT_STAMP(ln, 7);
+  if (itr) {
     if (yv >= ynew) {
       pd.px = q.x; pd.py = ynew; pd.pey = expshift(ynew, env.ymax); pd.pr = q.pr;
       pd.it++;
@@ -337,6 +349,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
     pend = false;
     ecs_jump_finish(P, ln, sk, st, f, xsamp, ainfo);
   }
+  PHT_STAMP(ln, 3);
 }
 
 }  // namespace pht

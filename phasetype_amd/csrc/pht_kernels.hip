@@ -216,6 +216,7 @@ ecs_exact_kernel(SweepArgs a) {
 #ifdef PHT_STAMPS
   ln.st_last = __builtin_amdgcn_s_memtime();
   for (int q = 0; q < 8; q++) ln.st_acc[q] = 0ull;
+  ln.st_rounds = 0ull;
 #endif
   EcsLane<NT> st;
   long pos = 0;
@@ -239,6 +240,8 @@ ecs_exact_kernel(SweepArgs a) {
   bool pend = false;
   for (;;) {
     bool need = false;
+    /* converged: generate the next Philox block ahead for the absorb tests */
+    if (have && !pend) pht_stream_topup(&ln.r);
     while (!done && !pend) {
       if (!have) {
         if (nextp >= a.count) {
@@ -283,11 +286,13 @@ ecs_exact_kernel(SweepArgs a) {
     }
     PHT_STAMP(ln, 0);
     if (!__any(need) && !__any(pend)) break;
+#ifdef PHT_STAMPS
+    ln.st_rounds++;
+#endif
 #if defined(PHT_ECS_NOFAST)
     if (need) ecs_jump(P, ln, env, sk, st);
 #elif defined(PHT_ECS_PEND)
     if (pend) pend = !ecs_jump_resume(P, ln, env, sk, st, pd);
-    PHT_STAMP(ln, 4);
     if (need) pend = !ecs_jump_start(P, ln, env, sk, st, &pd);
 #else
     ecs_round(P, ln, env, sk, st, need, pend, pd);
@@ -296,6 +301,7 @@ ecs_exact_kernel(SweepArgs a) {
 #ifdef PHT_STAMPS
   if ((threadIdx.x & 63) == 0)
     for (int q = 0; q < 8; q++) lds_add(&xc[8 + q], ln.st_acc[q]);
+  if ((threadIdx.x & 63) == 0) lds_add(&xc[6], ln.st_rounds);
 #endif
   __syncthreads();
   unsigned long long *g = a.stats;

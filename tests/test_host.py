@@ -247,8 +247,9 @@ def test_stream_uniforms_open_interval(orc):
                          out.ctypes.data_as(C.c_void_p))
     assert out.min() > 0.0 and out.max() < 1.0
     assert abs(out.mean() - 0.5) < 5 * np.sqrt(1 / 12 / len(out))
-    m = np.round(out * 2.0 ** 53)  # (2k+1) 2^-53: odd multiples
+    m = np.round(out * 2.0 ** 33)  # (2w+1) 2^-33: odd multiples (one 32-bit word per uniform)
     assert np.all(m % 2 == 1)
+    assert len(np.unique(out)) > 0.999 * len(out)
 
 
 def _ulp_err(got, x, fn):

@@ -25,9 +25,12 @@ zexp = P.zexp_for(y)
 sw.sweep(S, s, zexp=zexp)
 st = sw.sweep(S, s, key=(3, 4), zexp=zexp)
 ex = st[2 * a.n + a.n * a.n:]
-names = ["phaseA_refill_absorb", "arms_init", "arms_accept_tail", "movemass", "arms_reject_slowpath",
-         "arms_first_iteration"]
-tot = float(sum(ex[8:14]))
+names = ["phaseA_absorb_newobs", "start_evals_insert", "test_metropolis", "movemass_finish", "meets_cumulate",
+         "f0_cap", "invert", "proposal_eval"]
+tot = float(sum(ex[8:16]))
+rounds = float(ex[6])
 print(json.dumps({"kernel_ms": sw.last_kernel_ms(), "counters": ex[:8].tolist(),
-                  "shares": {k: float(v) / tot for k, v in zip(names, ex[8:14])},
+                  "wave_rounds": rounds,
+                  "cycles_per_round": {k: float(v) / max(rounds, 1) for k, v in zip(names, ex[8:16])},
+                  "shares": {k: float(v) / tot for k, v in zip(names, ex[8:16])},
                   "evals_per_jump": float(ex[1]) / max(1, ex[4]), "jumps_per_obs": float(ex[4]) / a.N}, indent=1))
