@@ -474,6 +474,23 @@ PHT_HD double pht_log(double x) {
   return (x != x || x <= 0.0 || x == INFINITY) ? spec : res;
 }
 
+/* Spectral dot product sum_i c_i e_i of the ECS path, in the order every
+ * implementation (one lane per observation, or G lanes sharing one) can
+ * reproduce: 16 residue slots p_r = c_r e_r (fma with c_{r+16} e_{r+16}
+ * for n > 16), then a pairwise tree p_r += p_{r+s} for s = 8, 4, 2, 1,
+ * adding only slots that exist (r + s < n). */
+PHT_HD double pht_dot16(const double *c, long cstride, const double *e, int n) {
+  double p[16];
+  for (int r = 0; r < 16; r++) {
+    p[r] = (r < n) ? c[r * cstride] * e[r] : 0.0;
+    if (r + 16 < n) p[r] = fma(c[(r + 16) * cstride], e[r + 16], p[r]);
+  }
+  for (int s = 8; s >= 1; s >>= 1)
+    for (int r = 0; r < s; r++)
+      if (r + s < n) p[r] = p[r] + p[r + s];
+  return p[0];
+}
+
 #if defined(__HIPCC__)
 /* copy the math tables into LDS (PHT_DETMATH_LDS); call at kernel entry,
  * before the first __syncthreads() */

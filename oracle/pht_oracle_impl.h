@@ -533,8 +533,9 @@ static double ORC_FN(ecs_dens)(double d, void *vctx) {
   const int n = sp->n, j = c->j;
 #if ORC_DEV
   /* log(sum_i W[j,i] e^{lambda_i (y_t - d)}) + S_jj d */
-  double x = c->y_t - d, acc = 0.0;
-  for (int i = 0; i < n; i++) acc = fma(sp->W[j + i * n], ORC_EXP_NEG(sp->evals[i] * x), acc);
+  double x = c->y_t - d, E[ORC_MAXN];
+  for (int i = 0; i < n; i++) E[i] = ORC_EXP_NEG(sp->evals[i] * x);
+  const double acc = pht_dot16(sp->W + j, n, E, n);
   return ORC_LOG(acc) + sp->S[j + j * n] * d;
 #else
   double pq[ORC_MAXN];
@@ -573,8 +574,9 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
     if (sp->s[j] > 0.0) {
       double U = ORC_FN(u)(rng), pab;
 #if ORC_DEV
-      double den = 0.0;
-      for (int i = 0; i < n; i++) den = fma(sp->QQs[j + i * n], ORC_EXP_NEG(sp->evals[i] * y_t), den);
+      double E0[ORC_MAXN];
+      for (int i = 0; i < n; i++) E0[i] = ORC_EXP_NEG(sp->evals[i] * y_t);
+      const double den = pht_dot16(sp->QQs + j, n, E0, n);
       pab = ORC_EXP(fma(sp->S[j + j * n], y_t, sp->logs[j]) - ORC_LOG(den));
 #else
       /* LJMA_probAbsorb (:120-136) */
@@ -610,8 +612,7 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
     for (int i = 0; i < n; i++) E[i] = ORC_EXP_NEG(sp->evals[i] * x);
     for (int q = 0; q < cnt; q++) {
       const int k = L[q];
-      double acc = 0.0;
-      for (int i = 0; i < n; i++) acc = fma(sp->QQs[k + i * n], E[i], acc);
+      const double acc = pht_dot16(sp->QQs + k, n, E, n);
       w[q] = sp->P[j + k * n] * acc;
       sum += w[q];
     }

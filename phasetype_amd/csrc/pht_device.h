@@ -92,6 +92,25 @@ struct Par {
 
 #define PHT_VEC(NT) ((NT) > 0 ? (NT) : kMaxN)
 
+/* pht_dot16 (include/pht_detmath.h) with coefficients read through an
+ * accessor cf(i): the ECS path's spectral dot products in spec order */
+template <class Cf>
+__device__ __forceinline__ double dev_dot16(const Cf &cf, const double *E, int n) {
+  double p[16];
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    p[r] = (r < n) ? cf(r) * E[r] : 0.0;
+    if (r + 16 < n) p[r] = fma(cf(r + 16), E[r + 16], p[r]);
+  }
+#pragma unroll
+  for (int s = 8; s >= 1; s >>= 1) {
+#pragma unroll
+    for (int r = 0; r < s; r++)
+      if (r + s < n) p[r] = p[r] + p[r + s];
+  }
+  return p[0];
+}
+
 /* division in the ARMS envelope code; PHT_FASTDIV_ABLATION is a timing-only
  * diagnostic build (approximate reciprocal: results differ) */
 #ifdef PHT_FASTDIV_ABLATION
@@ -732,20 +751,15 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
   __device__ __forceinline__ double operator()(double d) {
     const int n = P.n();
     const double x = y_t - d;
-    double acc = 0.0;
     if (haveE0 && d == 0.0) {
 #pragma unroll
-      for (int i = 0; i < n; i++) {
-        Elast[i] = E0[i];
-        acc = fma(P.W(j, i), E0[i], acc);
-      }
+      for (int i = 0; i < n; i++) Elast[i] = E0[i];
     } else {
 #pragma unroll
-      for (int i = 0; i < n; i++) {
-        Elast[i] = pht_exp_neg(P.evals(i) * x);
-        acc = fma(P.W(j, i), Elast[i], acc);
-      }
+      for (int i = 0; i < n; i++) Elast[i] = pht_exp_neg(P.evals(i) * x);
     }
+    const int jj = j;
+    const double acc = dev_dot16([&](int i) { return P.W(jj, i); }, Elast, n);
     lastd = d;
     return pht_log(acc) + Sjj * d;
   }
@@ -791,9 +805,7 @@ __device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink 
       for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
       st.haveE0 = true;
     }
-    double den = 0.0;
-#pragma unroll
-    for (int i = 0; i < n; i++) den = fma(P.QQs(j, i), st.E0[i], den);
+    const double den = dev_dot16([&](int i) { return P.QQs(j, i); }, st.E0, n);
     const double pab = pht_exp(fma(P.S(j, j), y_t, P.logs(j)) - pht_log(den));
     fin = (U < pab);
   }
@@ -838,9 +850,7 @@ __device__ __forceinline__ void ecs_jump_finish(const Par<NT> &P, Lane &ln, Sink
   for (int q = 0; q < PHT_VEC(NT); q++) {
     if (q < cnt) {
       const int k = P.succP(j, q);
-      double acc = 0.0;
-#pragma unroll
-      for (int i = 0; i < n; i++) acc = fma(P.QQs(k, i), E[i], acc);
+      const double acc = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
       w[q] = P.P(j, k) * acc;
       sum += w[q];
     }
