@@ -463,6 +463,24 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
 }
 
 /* enqueue one sweep (params already in c->h_params); stats -> c->h_stats */
+/* lanes per exact observation for the ECS kernel: PHT_GROUP=1|2|4|8 forces
+ * it; by default groups of 4 when the shard has few observations per lane
+ * (latency-bound regime), one lane otherwise.  Results are identical. */
+static int exact_group(const pht_ctx *c) {
+  if (const char *e = getenv("PHT_GROUP")) {
+    const int g = atoi(e);
+    return (g == 2 || g == 4 || g == 8) ? g : 0;
+  }
+  return 0;
+}
+
+/* blocks per CU for the persistent ECS kernel (PHT_ECS_OCC forces it) */
+static int exact_occ(const pht_ctx *c) {
+  if (const char *e = getenv("PHT_ECS_OCC")) return atoi(e);
+  (void)c;
+  return 0;
+}
+
 static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int zexp, bool debug) {
   HIPCHK(hipSetDevice(c->device));
   const int pb = make_layout(c->n).bytes();
@@ -512,6 +530,8 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     ae.begin = 0;
     ae.count = c->n_exact;
     ae.cens = nullptr;
+    ae.group = exact_group(c);
+    ae.occ = exact_occ(c);
     if (ae.count > 0) HIPCHK(pht_launch_sweep(&ae, c->method, debug ? 1 : 0, c->stream));
     SweepArgs ac = a;
     ac.begin = c->n_exact;

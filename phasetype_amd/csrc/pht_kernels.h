@@ -27,6 +27,8 @@ struct SweepArgs {
   uint32_t k0, k1, sweep;
   double zscale;               /* 2^zexp */
   unsigned long long *stats;   /* [stats_len(n)] int64, accumulated */
+  int group;                   /* ECS exact: lanes per observation (0/1 = one lane; 2, 4, 8) */
+  int occ;                     /* ECS exact: blocks per CU of the persistent grid (0 = occupancy limit) */
   /* debug per-observation outputs (DEBUG kernels only) */
   long long *dbg_zq;           /* [count*n] */
   int *dbg_N;                  /* [count*n*n] */

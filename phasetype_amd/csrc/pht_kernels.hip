@@ -18,6 +18,7 @@
 
 #include "pht_device.h"
 #include "pht_ecs_round.h"
+#include "pht_ecs_group.h"
 #include "pht_env.h"
 #include "pht_kernels.h"
 
@@ -342,17 +343,183 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
     occ = b;
   }
   long want = (a.count + kBlock - 1) / kBlock;
-  long grid = (long)cus * occ;
+  /* blocks per CU: the occupancy limit, or fewer (a.occ) when the shard is
+   * small and the longest paths, not throughput, set the time */
+  const int bpc = (a.occ > 0 && a.occ < occ) ? a.occ : occ;
+  long grid = (long)cus * bpc;
   if (grid > want) grid = want;
   if (grid < 1) return hipSuccess;
   hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
   return hipGetLastError();
 }
 
+/*
+ * ECS exact observations, G lanes per observation (pht_ecs_group.h): the
+ * same persistent scheme as ecs_exact_kernel with groups in place of lanes
+ * (block b's groups take positions b, b + grid, ... through the LDS cursor).
+ */
+template <int NT, int G, bool DEBUG>
+__global__ void __launch_bounds__(kBlock) ecs_group_kernel(SweepArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int n = nval<NT>(a.n);
+  const Layout L = make_layout(n);
+  const int pbytes = L.bytes();
+  {
+    const unsigned long long *src = reinterpret_cast<const unsigned long long *>(a.params);
+    PHT_LDS unsigned long long *dst = (PHT_LDS unsigned long long *)smem;
+    for (int k = threadIdx.x; k < pbytes / 8; k += blockDim.x) dst[k] = src[k];
+  }
+  PHT_LDS unsigned char *lsm = (PHT_LDS unsigned char *)smem;
+  PHT_LDS unsigned long long *zq = (PHT_LDS unsigned long long *)(lsm + pbytes);
+  PHT_LDS unsigned long long *xc = zq + n;
+  PHT_LDS unsigned *Bc = (PHT_LDS unsigned *)(xc + kStatExtra);
+  PHT_LDS unsigned *Nc = Bc + n;
+  PHT_LDS int *cursor = (PHT_LDS int *)(Nc + n * n);
+  PHT_LDS double *genv = (PHT_LDS double *)(lsm + ((pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 15) & ~15));
+  pht_stage_math_tables();
+  for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
+  for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
+  if (threadIdx.x == 0) *cursor = 0;
+  __syncthreads();
+
+  Par<NT> P;
+  P.d = (const PHT_LDS double *)lsm;
+  P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
+  P.Lr = L;
+  const int gl = threadIdx.x % G, grp = threadIdx.x / G;
+  GEnv env;
+  env.x = genv + grp * 5 * kGrpArr;
+  env.y = env.x + kGrpArr;
+  env.ey = env.y + kGrpArr;
+  env.ar = env.ey + kGrpArr;
+  env.cum = env.ar + kGrpArr;
+  env.cnt = 0;
+  env.ymax = 0.0;
+  EnvPrivate benv;
+  Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
+  Lane ln;
+  GState<NT, G> st;
+  ArmsPend pd;
+  bool pend = false, big = false;
+  long pos = 0;
+  bool have = false, done = false;
+  auto claim = [&]() -> long {
+    int v = 0;
+    if (gl == 0) v = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    v = __shfl(v, 0, G);
+    return blockIdx.x + (long)v * gridDim.x;
+  };
+  long nextp = claim();
+  double ny = 0.0;
+  uint32_t ngid = 0;
+  if (nextp < a.count) {
+    ny = a.y[a.begin + nextp];
+    ngid = a.gid[a.begin + nextp];
+  }
+  for (;;) {
+    bool need = false;
+    if (have && !pend) pht_stream_topup(&ln.r);
+    while (!done && !pend) {
+      if (!have) {
+        if (nextp >= a.count) {
+          done = true;
+          break;
+        }
+        pos = a.begin + nextp;
+        const double yobs = ny;
+        const uint32_t gobs = ngid;
+        nextp = claim();
+        if (nextp < a.count) {
+          ny = a.y[a.begin + nextp];
+          ngid = a.gid[a.begin + nextp];
+        }
+        pht_stream_init(&ln.r, a.k0, a.k1, gobs, 0u, a.sweep);
+        ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
+        if (DEBUG) {
+          sk.dz = a.dbg_zq + pos * n;
+          sk.dN = a.dbg_N + pos * n * n;
+          sk.dB = a.dbg_B + pos;
+          sk.dpre = a.dbg_pre + pos;
+        }
+        {
+          const double target = dev_u(ln.r);
+          const int B = pistart(P, target, ln.flags);
+          if (gl == 0) sk.start(B);
+          st.yt = yobs;
+          st.j = B;
+          st.njump = 0;
+          st.haveE0 = false;
+        }
+        have = true;
+      }
+      if (g_try_absorb<NT, G>(P, ln, sk, st, gl)) {
+        const uint32_t nd = pht_stream_pos(&ln.r);
+        if (gl == 0) {
+          if (DEBUG) {
+            a.dbg_flags[pos] = ln.flags;
+            a.dbg_ndraw[pos] = nd;
+          }
+          lds_add(&xc[0], 1ull);
+          lds_add(&xc[1], (unsigned long long)ln.neval);
+          if (ln.flags) lds_add(&xc[2], 1ull);
+          lds_add(&xc[3], (unsigned long long)nd);
+          lds_add(&xc[4], (unsigned long long)ln.njump);
+        }
+        have = false;
+        continue;
+      }
+      need = true;
+      break;
+    }
+    if (!__any(need) && !__any(pend)) break;
+    g_round<NT, G>(P, ln, env, benv, sk, st, need, pend, big, pd, gl);
+  }
+  __syncthreads();
+  unsigned long long *g = a.stats;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    if (zq[k]) atomicAdd(&g[k], zq[k]);
+    if (Bc[k]) atomicAdd(&g[n + k], (unsigned long long)Bc[k]);
+  }
+  for (int k = threadIdx.x; k < n * n; k += blockDim.x)
+    if (Nc[k]) atomicAdd(&g[2 * n + k], (unsigned long long)Nc[k]);
+  for (int k = threadIdx.x; k < kStatExtra; k += blockDim.x)
+    if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
+}
+
+template <int NT, int G, bool DEBUG>
+static hipError_t launch_ecs_group(const SweepArgs &a, hipStream_t st) {
+  static int occ = -1, cus = 0;
+  const int sm = ((smem_bytes(a.n) + 4 + 15) & ~15) + (kBlock / G) * 5 * kGrpArr * 8;
+  if (occ < 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
+    cus = prop.multiProcessorCount;
+    if (hipFuncSetAttribute((const void *)ecs_group_kernel<NT, G, DEBUG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            sm) != hipSuccess)
+      return hipErrorUnknown;
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, ecs_group_kernel<NT, G, DEBUG>, kBlock, sm) != hipSuccess ||
+        b < 1)
+      b = 1;
+    occ = b;
+  }
+  long want = (a.count + (kBlock / G) - 1) / (kBlock / G);
+  long grid = (long)cus * occ;
+  if (grid > want) grid = want;
+  if (grid < 1) return hipSuccess;
+  hipLaunchKernelGGL((ecs_group_kernel<NT, G, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
+  return hipGetLastError();
+}
+
 template <int NT>
 static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStream_t st) {
-  if (method == kMethodECS && a.cens == nullptr) /* exact-only range */
+  if (method == kMethodECS && a.cens == nullptr) { /* exact-only range */
+    if (a.group == 4) return debug ? launch_ecs_group<NT, 4, true>(a, st) : launch_ecs_group<NT, 4, false>(a, st);
+    if (a.group == 2) return debug ? launch_ecs_group<NT, 2, true>(a, st) : launch_ecs_group<NT, 2, false>(a, st);
+    if (a.group == 8) return debug ? launch_ecs_group<NT, 8, true>(a, st) : launch_ecs_group<NT, 8, false>(a, st);
     return debug ? launch_ecs_exact<NT, true>(a, st) : launch_ecs_exact<NT, false>(a, st);
+  }
   const int blocks = (int)((a.count + kBlock - 1) / kBlock);
   if (blocks == 0) return hipSuccess;
   const int sm = smem_bytes(a.n);

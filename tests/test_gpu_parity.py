@@ -127,3 +127,38 @@ def test_statistical_vs_reference(gpu, ref):
         ng, nr = g["N"].reshape(N, -1).astype(float), Nr.reshape(N, -1).astype(float)
         se = np.sqrt(nr.var(0) / N + ng.var(0) / N) + 1e-12
         assert np.all(np.abs(nr.mean(0) - ng.mean(0)) < 5 * se + 1e-9), method
+
+
+@pytest.mark.parametrize("group,n,cf", [(4, 10, 0.0), (2, 5, 0.3), (8, 3, 0.0), (4, 15, 0.3)])
+def test_group_kernel_bitexact(gpu, orc, monkeypatch, group, n, cf):
+    """The ECS-exact kernel with G lanes per observation (pht_ecs_group.h,
+    PHT_GROUP=G) gives the one-lane results bit for bit."""
+    monkeypatch.setenv("PHT_GROUP", str(group))
+    S0, s0 = bd_exit(n)
+    y, cen = simulate_ph(S0, s0, 3000, seed=2000 + n, censor_frac=cf)
+    S, s = _perturbed(n, n + 1)
+    zexp = int(orc.lib.orc_zexp(np.ascontiguousarray(y), len(y)))
+    o = orc.dev_sweep(2, S, s, y, cen, key=(11, 22), sweep=3, zexp=zexp)
+    sw = P.Sweeper(n, 2, 1)
+    sw.set_obs(y, cen)
+    g = sw.sweep_debug(S, s, key=(11, 22), sweep=3, zexp=zexp)
+    for f in ("B", "pre", "flags", "ndraw"):
+        assert np.array_equal(g[f], o[f]), f
+    assert np.array_equal(g["zq"], o["zq"]) and np.array_equal(g["N"], o["N"])
+    st = sw.sweep(S, s, key=(11, 22), sweep=3, zexp=zexp)
+    assert np.array_equal(st[:2 * n + n * n], g["stats"][:2 * n + n * n])
+
+
+@pytest.mark.parametrize("occ", [1, 2])
+def test_grid_occupancy_invariance(gpu, monkeypatch, occ):
+    """Blocks per CU of the persistent kernel (PHT_ECS_OCC) change nothing."""
+    n = 10
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 20000, seed=31)
+    zexp = P.zexp_for(y)
+    sw = P.Sweeper(n, 2)
+    sw.set_obs(y, cen)
+    ref = sw.sweep(S, s, key=(1, 9), sweep=2, zexp=zexp)
+    monkeypatch.setenv("PHT_ECS_OCC", str(occ))
+    got = sw.sweep(S, s, key=(1, 9), sweep=2, zexp=zexp)
+    assert np.array_equal(ref[:2 * n + n * n], got[:2 * n + n * n])
