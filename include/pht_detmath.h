@@ -474,6 +474,29 @@ PHT_HD double pht_log(double x) {
   return (x != x || x <= 0.0 || x == INFINITY) ? spec : res;
 }
 
+/* e^u for |u| <= 2^-8 (degree-5 Taylor, truncation < 2^-60 relative) */
+PHT_HD double pht_exp_taylor(double u) {
+  double q = 8.3333333333333332177e-03;      /* 1/5! */
+  q = fma(q, u, 4.1666666666666664354e-02);  /* 1/4! */
+  q = fma(q, u, 1.6666666666666665741e-01);  /* 1/3! */
+  q = fma(q, u, 0.5);
+  q = fma(q, u, 1.0);
+  return fma(q, u, 1.0);
+}
+
+/* Exponential vectors of the four ARMS starting points of an ECS sojourn
+ * (xinit = {a, b, 2b, y_t - a}, a = y_t/1e6, b = y_t/3; the density at d
+ * needs e^{lambda_i (y_t - d)}):
+ *   point 2b : e^{lambda (y_t - 2b)} directly          (F)
+ *   point b  : F^2                                       (y_t - b ~ 2 (y_t - 2b))
+ *   point a  : e^{lambda y_t} * taylor(-lambda a)        (E0 is known)
+ *   point y_t - a : taylor(lambda (y_t - (y_t - a)))
+ * used when max|lambda| * max(a, y_t - (y_t - a)) <= 2^-8, else direct
+ * exponentials for all four.  Returns whether the identities were used. */
+PHT_HD int pht_ecs_init_ok(double lammax, double a, double x3) {
+  return lammax * (a > x3 ? a : x3) <= 0x1p-8;
+}
+
 /* Spectral dot product sum_i c_i e_i of the ECS path, in the order every
  * implementation (one lane per observation, or G lanes sharing one) can
  * reproduce: 16 residue slots p_r = c_r e_r (fma with c_{r+16} e_{r+16}

@@ -234,8 +234,12 @@ static void ORC_FN(update)(ORC_FN(env) *e, const ORC_FN(wpt) *p, orc_dens f, voi
  * src/Simulate_AbsCTMC_gt_Aslett_DCS.c:227-250).  Returns the error code
  * and writes the sample (left at 0 on error, as the callers' xsamp=0).
  */
+/* optional evaluator of the four starting points at once (device spec of
+ * the ECS sojourn density, pht_detmath.h pht_ecs_init_ok); NULL: f each */
+typedef void (*orc_dens_init)(const double xinit[4], double y[4], void *ctx);
+
 static int ORC_FN(arms)(const double xinit[4], double xl, double xr, orc_dens f, void *ctx,
-                        double xprev, double *xsamp, ORC_FN(rng) *rng, int *neval_out) {
+                        double xprev, double *xsamp, ORC_FN(rng) *rng, int *neval_out, orc_dens_init finit) {
   ORC_FN(env) e;
   e.convex = 1.0;
   e.neval = 0;
@@ -244,9 +248,11 @@ static int ORC_FN(arms)(const double xinit[4], double xl, double xr, orc_dens f,
     if (xinit[i] <= xinit[i - 1]) return 1004;
   e.cnt = 9;
   e.x[0] = xl;
+  double yi[4];
+  if (finit) finit(xinit, yi, ctx);
   for (int k = 0; k < 4; k++) {
     e.x[2 * k + 1] = xinit[k];
-    e.y[2 * k + 1] = f(xinit[k], ctx);
+    e.y[2 * k + 1] = finit ? yi[k] : f(xinit[k], ctx);
     e.neval++;
   }
   e.x[8] = xr;
@@ -526,6 +532,10 @@ typedef struct {
   const double *p; /* ref: rate row p_j (p_jj = 0) */
 } ORC_FN(ecs_ctx);
 
+#if ORC_DEV
+/* the four starting points of an ECS sojourn (device spec, pht_detmath.h) */
+static void ORC_FN(ecs_init4)(const double xinit[4], double yv[4], void *vctx);
+#endif
 /* LJMA_ECS_dens (src/Simulate_AbsCTMC_eq_Aslett_ECS.c:150-171) */
 static double ORC_FN(ecs_dens)(double d, void *vctx) {
   ORC_FN(ecs_ctx) *c = (ORC_FN(ecs_ctx) *)vctx;
@@ -546,6 +556,33 @@ static double ORC_FN(ecs_dens)(double d, void *vctx) {
   return ORC_LOG(term1) + sp->S[j + j * n] * d;
 #endif
 }
+
+#if ORC_DEV
+static void ORC_FN(ecs_init4)(const double xinit[4], double yv[4], void *vctx) {
+  ORC_FN(ecs_ctx) *c = (ORC_FN(ecs_ctx) *)vctx;
+  const orc_sp *sp = c->sp;
+  const int n = sp->n, j = c->j;
+  const double y_t = c->y_t;
+  double lammax = 0.0;
+  for (int i = 0; i < n; i++) lammax = fmax(lammax, fabs(sp->evals[i]));
+  const double x3 = y_t - xinit[3];
+  double E[4][ORC_MAXN];
+  if (pht_ecs_init_ok(lammax, xinit[0], x3)) {
+    for (int i = 0; i < n; i++) {
+      const double F = ORC_EXP_NEG(sp->evals[i] * (y_t - xinit[2]));
+      E[2][i] = F;
+      E[1][i] = F * F;
+      E[0][i] = ORC_EXP_NEG(sp->evals[i] * y_t) * pht_exp_taylor(-sp->evals[i] * xinit[0]);
+      E[3][i] = pht_exp_taylor(sp->evals[i] * x3);
+    }
+  } else {
+    for (int k = 0; k < 4; k++)
+      for (int i = 0; i < n; i++) E[k][i] = ORC_EXP_NEG(sp->evals[i] * (y_t - xinit[k]));
+  }
+  for (int k = 0; k < 4; k++)
+    yv[k] = ORC_LOG(pht_dot16(sp->W + j, n, E[k], n)) + sp->S[j + j * n] * xinit[k];
+}
+#endif
 
 /* LJMA_samplechain_Aslett2 (src/Simulate_AbsCTMC_eq_Aslett_ECS.c:205-373) */
 static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_obs *o,
@@ -597,7 +634,11 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
     xinit[2] = xinit[1] * 2.0;
     xinit[3] = y_t - xinit[0];
     double xsamp = 0.0;
-    int ainfo = ORC_FN(arms)(xinit, 0.0, y_t, ORC_FN(ecs_dens), &ctx, 0.0, &xsamp, rng, neval);
+    #if ORC_DEV
+    int ainfo = ORC_FN(arms)(xinit, 0.0, y_t, ORC_FN(ecs_dens), &ctx, 0.0, &xsamp, rng, neval, ORC_FN(ecs_init4));
+#else
+    int ainfo = ORC_FN(arms)(xinit, 0.0, y_t, ORC_FN(ecs_dens), &ctx, 0.0, &xsamp, rng, neval, NULL);
+#endif
     if (ainfo) o->flags |= (ainfo == 4) ? 4 : 32;
     t += d = xsamp;
     /* LJMA_moveMass (:21-41) then the categorical draw (:352-358) */
@@ -707,7 +748,7 @@ static double ORC_FN(condjump)(const orc_sp *sp, double tnow, int jnow, double y
   xinit[2] = xinit[1] * 2.0;
   xinit[3] = y - tnow - xinit[0];
   double xsamp = 0.0;
-  int ainfo = ORC_FN(arms)(xinit, 0.0, y - tnow, ORC_FN(cj_dens), &ctx, 0.0, &xsamp, rng, neval);
+  int ainfo = ORC_FN(arms)(xinit, 0.0, y - tnow, ORC_FN(cj_dens), &ctx, 0.0, &xsamp, rng, neval, NULL);
   if (ainfo) *flags |= (ainfo == 4) ? 4 : 32;
   return xsamp;
 }

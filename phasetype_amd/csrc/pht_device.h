@@ -489,10 +489,20 @@ __device__ __forceinline__ int arms(Env &e, const double xinit[4], double xl, do
   if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) return 1004;
   e.cnt = 9;
   e.sX(0, xl);
+  if constexpr (F::kInit4) {
+    double yv[4];
+    f.init4(xinit, yv);
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    e.sX(2 * k + 1, xinit[k]);
-    e.sY(2 * k + 1, f(xinit[k]));
+    for (int k = 0; k < 4; k++) {
+      e.sX(2 * k + 1, xinit[k]);
+      e.sY(2 * k + 1, yv[k]);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      e.sX(2 * k + 1, xinit[k]);
+      e.sY(2 * k + 1, f(xinit[k]));
+    }
   }
   ln.neval += 4;
   e.sX(8, xr);
@@ -641,10 +651,17 @@ __device__ __forceinline__ int arms_fast(Env &slow, const double xinit[4], doubl
   Env9 e;
   e.x[0] = xl;
   e.y[0] = 0.0;
+  double yi[4];
+  if constexpr (F::kInit4) {
+    f.init4(xinit, yi);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) yi[k] = f(xinit[k]);
+  }
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     e.x[2 * k + 1] = xinit[k];
-    e.y[2 * k + 1] = f(xinit[k]);
+    e.y[2 * k + 1] = yi[k];
     e.x[2 * k + 2] = 0.0;
     e.y[2 * k + 2] = 0.0;
   }
@@ -762,6 +779,44 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
     const double acc = dev_dot16([&](int i) { return P.W(jj, i); }, Elast, n);
     lastd = d;
     return pht_log(acc) + Sjj * d;
+  }
+  /* the four ARMS starting points at once (device spec: pht_ecs_init_ok in
+   * include/pht_detmath.h; oracle orcD_ecs_init4) */
+  static constexpr bool kInit4 = true;
+  __device__ __forceinline__ void init4(const double xinit[4], double yv[4]) {
+    const int n = P.n();
+    const int jj = j;
+    auto Wj = [&](int i) { return P.W(jj, i); };
+    double lammax = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; i++) lammax = fmax(lammax, fabs(P.evals(i)));
+    const double x3 = y_t - xinit[3];
+    double acc[4];
+    if (pht_ecs_init_ok(lammax, xinit[0], x3)) {
+      double F[PHT_VEC(NT)], T[PHT_VEC(NT)];
+#pragma unroll
+      for (int i = 0; i < n; i++) F[i] = pht_exp_neg(P.evals(i) * (y_t - xinit[2]));
+      acc[2] = dev_dot16(Wj, F, n);
+#pragma unroll
+      for (int i = 0; i < n; i++) T[i] = F[i] * F[i];
+      acc[1] = dev_dot16(Wj, T, n);
+#pragma unroll
+      for (int i = 0; i < n; i++) T[i] = E0[i] * pht_exp_taylor(-P.evals(i) * xinit[0]);
+      acc[0] = dev_dot16(Wj, T, n);
+#pragma unroll
+      for (int i = 0; i < n; i++) Elast[i] = pht_exp_taylor(P.evals(i) * x3);
+      acc[3] = dev_dot16(Wj, Elast, n);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+#pragma unroll
+        for (int i = 0; i < n; i++) Elast[i] = pht_exp_neg(P.evals(i) * (y_t - xinit[k]));
+        acc[k] = dev_dot16(Wj, Elast, n);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) yv[k] = pht_log(acc[k]) + Sjj * xinit[k];
+    lastd = xinit[3];
   }
 };
 
@@ -945,6 +1000,8 @@ __device__ __forceinline__ void ecs_exact(const Par<NT> &P, double y, Lane &ln, 
 /* ===================================================== censored path */
 template <int NT>
 struct CjDens { /* log F_{P_j}(y - t - d) + log dexp(d; 1/-S_jj) */
+  static constexpr bool kInit4 = false;
+  __device__ __forceinline__ void init4(const double *, double *) {}
   const Par<NT> &P;
   int j;
   double tnow, y, scale, logscale;

@@ -115,6 +115,41 @@ struct GDens {
     return gdot16<NT, G>([&](int i) { return P.W(jj, i); }, El, gl, n);
   }
   __device__ __forceinline__ double operator()(double d) { return pht_log(eval_acc(d)) + Sjj * d; }
+  /* EcsDens::init4 on slices: the four sums (every lane gets all four) */
+  __device__ __forceinline__ void init4_acc(const double xinit[4], double acc[4]) {
+    const int n = P.n();
+    const int jj = j;
+    auto Wj = [&](int i) { return P.W(jj, i); };
+    double lammax = 0.0;
+    for (int i = 0; i < n; i++) lammax = fmax(lammax, fabs(P.evals(i)));
+    const double x3 = y_t - xinit[3];
+    if (pht_ecs_init_ok(lammax, xinit[0], x3)) {
+      double F[SL::S], T[SL::S];
+      gexp<NT, G>(P, y_t - xinit[2], F, gl, n);
+      acc[2] = gdot16<NT, G>(Wj, F, gl, n);
+#pragma unroll
+      for (int s = 0; s < SL::S; s++) T[s] = F[s] * F[s];
+      acc[1] = gdot16<NT, G>(Wj, T, gl, n);
+#pragma unroll
+      for (int h = 0; h < SL::H; h++)
+#pragma unroll
+        for (int q = 0; q < SL::Q; q++) {
+          const int i = gl + G * q + 16 * h;
+          const double lam = (i < n) ? P.evals(i) : 0.0;
+          T[h * SL::Q + q] = E0[h * SL::Q + q] * pht_exp_taylor(-lam * xinit[0]);
+          El[h * SL::Q + q] = pht_exp_taylor(lam * x3);
+        }
+      acc[0] = gdot16<NT, G>(Wj, T, gl, n);
+      acc[3] = gdot16<NT, G>(Wj, El, gl, n);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        gexp<NT, G>(P, y_t - xinit[k], El, gl, n);
+        acc[k] = gdot16<NT, G>(Wj, El, gl, n);
+      }
+    }
+    lastd = xinit[3];
+  }
 };
 
 /* per-group envelope in LDS */
@@ -447,8 +482,7 @@ __device__ __forceinline__ void g_round(const Par<NT> &P, Lane &ln, GEnv &env, E
       fin = true;
     } else {
       double acc[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) acc[k] = f.eval_acc(xinit[k]);
+      f.init4_acc(xinit, acc);
       ln.neval += 4;
       env.cnt = 9;
 #pragma unroll

@@ -262,10 +262,12 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
     } else {
       env.cnt = 9;
       env.sX(0, 0.0);
+      double yv[4];
+      f.init4(xinit, yv);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         env.sX(2 * k + 1, xinit[k]);
-        env.sY(2 * k + 1, f(xinit[k]));
+        env.sY(2 * k + 1, yv[k]);
       }
       ln.neval += 4;
       env.sX(8, y_t);
