@@ -89,9 +89,10 @@ __device__ __forceinline__ void round_meets(Env &e, int last) {
   if constexpr (CAP > 11) round_meet<12, CAP>(e, last);
 }
 
-/* arms_cumulate over the first CAP positions (cnt <= CAP) */
+/* arms_cumulate over the first CAP positions (cnt <= CAP); the cumulative
+ * areas go to cs[] (registers), not to the envelope */
 template <int CAP, class Env>
-__device__ __forceinline__ void round_cumulate(Env &e) {
+__device__ __forceinline__ void round_cumulate(Env &e, double *cs) {
   const int cnt = e.cnt;
   double xs[CAP], ys[CAP];
 #pragma unroll
@@ -105,7 +106,7 @@ __device__ __forceinline__ void round_cumulate(Env &e) {
   e.ymax = ymax;
   double eyp = expshift(ys[0], ymax);
   double cum = 0.;
-  e.sCUM(0, cum);
+  cs[0] = cum;
 #pragma unroll
   for (int k = 1; k < CAP; k++) {
     const double xp = xs[k - 1], xk = xs[k], yp = ys[k - 1], yk = ys[k];
@@ -114,19 +115,21 @@ __device__ __forceinline__ void round_cumulate(Env &e) {
     const double ex = (PHT_DIV((eyk - eyp), (yk - yp))) * (xk - xp);
     const double a = (xp == xk) ? 0. : ((fabs(yk - yp) < kYEps) ? lin : ex);
     cum = cum + a;
-    e.sCUM(k, cum);
+    cs[k] = cum;
     eyp = eyk;
   }
 }
 
-/* arms_invert with the unrolled scan; ey of the two segment ends recomputed */
+/* arms_invert with the unrolled scan over cs[] (registers); the segment's
+ * ends are tracked along the scan; ey of the two ends recomputed */
 template <int CAP, class Env>
-__device__ __forceinline__ void round_invert(Env &e, double prob, WPt &p) {
+__device__ __forceinline__ void round_invert(Env &e, const double *cs, double prob, WPt &p) {
   const int last = e.cnt - 1;
-  double cs[CAP];
+  double clast = cs[0];
 #pragma unroll
-  for (int k = 0; k < CAP; k++) cs[k] = e.CUM(k);
-  const double u = prob * e.CUM(last);
+  for (int k = 1; k < CAP; k++) clast = (k == last) ? cs[k] : clast;
+  const double u = prob * clast;
+  /* q moves down from last while cum[q-1] > u */
   int q = last;
   bool go = true;
 #pragma unroll
@@ -136,8 +139,13 @@ __device__ __forceinline__ void round_invert(Env &e, double prob, WPt &p) {
       q = go ? k : q;
     }
   }
+  double cr = cs[0], cl = cs[0];
+#pragma unroll
+  for (int k = 1; k < CAP; k++) {
+    cr = (k == q) ? cs[k] : cr;
+    cl = (k == q) ? cs[k - 1] : cl;
+  }
   p.pr = q;
-  const double cr = e.CUM(q), cl = e.CUM(q - 1);
   const double prop = PHT_DIV((u - cl), (cr - cl));
   const double xl = e.X(q - 1), xr = e.X(q);
   const double yr = e.Y(q), yl = e.Y(q - 1);
@@ -285,16 +293,17 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
    * the wavefront (9, 11 or 13 points) */
   const bool arm = (start && !fin) || (pend && !big);
   const int cap = __any(arm && env.cnt > 11) ? 13 : (__any(arm && env.cnt > 9) ? 11 : 9);
+  double cs[kRoundCap]; /* cumulative areas, cumulate -> invert */
   if (arm) {
     if (cap == 9) {
       round_meets<9>(env, env.cnt - 1);
-      round_cumulate<9>(env);
+      round_cumulate<9>(env, cs);
     } else if (cap == 11) {
       round_meets<11>(env, env.cnt - 1);
-      round_cumulate<11>(env);
+      round_cumulate<11>(env, cs);
     } else {
       round_meets<13>(env, env.cnt - 1);
-      round_cumulate<13>(env);
+      round_cumulate<13>(env, cs);
     }
   }
   PHT_STAMP(ln, 4);
@@ -316,9 +325,9 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
   double yv = 0.0, ynew = 0.0;
   if (itr) {
     const double pu = dev_u(ln.r);
-    if (cap == 9) round_invert<9>(env, pu, q);
-    else if (cap == 11) round_invert<11>(env, pu, q);
-    else round_invert<13>(env, pu, q);
+    if (cap == 9) round_invert<9>(env, cs, pu, q);
+    else if (cap == 11) round_invert<11>(env, cs, pu, q);
+    else round_invert<13>(env, cs, pu, q);
     const double u = dev_u(ln.r) * q.ey;
     yv = logshift(u, env.ymax);
   }

@@ -72,5 +72,34 @@ struct EnvLds {
   }
 };
 
+/* x and y of the first K points per lane in LDS (lane-interleaved), the
+ * rest and all of cum in private memory.  The converged ECS round keeps cum
+ * in registers between cumulate and invert and never touches the private
+ * part for envelopes of up to K points; the general ARMS code (rare, long
+ * rejection chains) uses the full accessors. */
+template <int K, int STRIDE>
+struct EnvLdsXY {
+  static constexpr int kSpill = 100 - K;
+  PHT_LDS double *l;   /* lane's element 0 */
+  PHT_PRIV double *ov; /* [2][kSpill] x, y beyond K */
+  PHT_PRIV double *cm; /* [100] cum */
+  int cnt;
+  double ymax;
+  __device__ __forceinline__ void bind(PHT_LDS double *lds, int tid, PHT_PRIV double *spill, PHT_PRIV double *cum) {
+    l = lds + tid;
+    ov = spill;
+    cm = cum;
+  }
+  static constexpr int lds_doubles_per_lane() { return 2 * K; }
+  __device__ __forceinline__ double X(int k) const { if (k < K) return l[k * STRIDE]; return ov[k - K]; }
+  __device__ __forceinline__ double Y(int k) const { if (k < K) return l[(K + k) * STRIDE]; return ov[kSpill + k - K]; }
+  __device__ __forceinline__ double CUM(int k) const { return cm[k]; }
+  __device__ __forceinline__ void sX(int k, double v) { if (k < K) l[k * STRIDE] = v; else ov[k - K] = v; }
+  __device__ __forceinline__ void sY(int k, double v) {
+    if (k < K) l[(K + k) * STRIDE] = v; else ov[kSpill + k - K] = v;
+  }
+  __device__ __forceinline__ void sCUM(int k, double v) { cm[k] = v; }
+};
+
 }  // namespace pht
 #endif

@@ -160,7 +160,7 @@ static int smem_bytes(int n) {
 #endif
 constexpr int kEnvK = PHT_ENV_K;
 #ifndef PHT_SLOW_K
-#define PHT_SLOW_K 10
+#define PHT_SLOW_K 15
 #endif
 
 #ifndef PHT_ECS_WAVES
@@ -203,11 +203,13 @@ ecs_exact_kernel(SweepArgs a) {
   double spill[3 * EnvLds<kEnvK, kBlock>::kSpill];
   env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill);
 #elif PHT_SLOW_K > 0
-  /* fresh envelopes live in registers (arms_fast); updated ones (after a
-   * rejection) in LDS, lane-interleaved, points >= PHT_SLOW_K in scratch */
-  EnvLds<PHT_SLOW_K, kBlock> env;
-  double spill[3 * EnvLds<PHT_SLOW_K, kBlock>::kSpill];
-  env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill);
+  /* the envelope's x and y in LDS (lane-interleaved) up to PHT_SLOW_K
+   * points; cum lives in registers within a round (pht_ecs_round.h) and in
+   * private memory for the general ARMS code */
+  EnvLdsXY<PHT_SLOW_K, kBlock> env;
+  double spill[2 * EnvLdsXY<PHT_SLOW_K, kBlock>::kSpill];
+  double cumv[100];
+  env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill, (PHT_PRIV double *)cumv);
 #else
   (void)envl;
   EnvPrivate env;
@@ -320,7 +322,7 @@ static int smem_bytes_ecs(int n) {
 #ifdef PHT_ECS_NOFAST
   return ((smem_bytes(n) + 4 + 15) & ~15) + EnvLds<kEnvK, kBlock>::lds_doubles_per_lane() * 8 * kBlock;
 #else
-  return ((smem_bytes(n) + 4 + 15) & ~15) + 3 * PHT_SLOW_K * 8 * kBlock;
+  return ((smem_bytes(n) + 4 + 15) & ~15) + 2 * PHT_SLOW_K * 8 * kBlock;
 #endif
 }
 

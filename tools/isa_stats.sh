@@ -30,7 +30,8 @@ for blk in re.finditer(r"^(_Z\S+):[^\n]*\n(.*?)\.Lfunc_end", s, re.S | re.M):
     if "ecs_exact" in name and "Lb0" in name:
         for op, c in ops.most_common(30):
             print(f"   {op:28s} {c}")
-for key in ("NumVgprs", "NumSgprs", "ScratchSize", "Occupancy", "LDSByteSize"):
-    vals = re.findall(rf"; {key}: (\d+)", s)
-    print(key, vals)
+# per-kernel resources (the comment block after each function body)
+for m in re.finditer(r"^(_Z\S+):[^\n]*\n(.*?)\.Lfunc_end.*?; NumVgprs: (\d+).*?; ScratchSize: (\d+).*?; Occupancy: (\d+)",
+                     s, re.S | re.M):
+    print(f"  {m.group(1)[:60]:60s} vgpr {m.group(3):>4s} scratch {m.group(4):>5s} occ {m.group(5)}")
 EOF
