@@ -62,6 +62,15 @@ struct Sink {
 template <int NT>
 __device__ __forceinline__ int nval(int n) { return NT > 0 ? NT : n; }
 
+/* Position of a block's t-th claim in the persistent kernels: chunks of
+ * kClaimChunk consecutive positions, block b taking chunks b, b + grid, ...
+ * (the sorted order is walked by all blocks together; a wavefront's claims
+ * are contiguous, so its y/gid loads coalesce).  Increasing in t. */
+constexpr int kClaimChunk = 64;
+__device__ __forceinline__ long claim_pos(long t) {
+  return ((t / kClaimChunk) * (long)gridDim.x + blockIdx.x) * kClaimChunk + (t % kClaimChunk);
+}
+
 template <int NT, int METHOD, bool DEBUG, class Env>
 __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -148,9 +157,9 @@ static int smem_bytes(int n) {
 }
 
 /*
- * ECS exact observations, persistent lanes.  Block b owns positions
- * b, b + G, b + 2G, ... of the launch range (G = grid size) and hands them
- * to its lanes through an LDS cursor: a lane that finishes a path takes the
+ * ECS exact observations, persistent lanes.  Block b owns chunks of 64
+ * positions (claim_pos) of the launch range and hands them to its lanes
+ * through an LDS cursor: a lane that finishes a path takes the
  * next observation at once, so the expensive ARMS phase runs with (almost)
  * all lanes of a wavefront active instead of waiting for the longest path.
  * The ARMS envelope lives in LDS (EnvLds<kEnvK>), lane-interleaved.
@@ -227,8 +236,8 @@ ecs_exact_kernel(SweepArgs a) {
   /* the lane's next observation is claimed and its (y, gid) loaded one
    * observation ahead, so a refill never waits on global memory */
   auto claim = [&]() -> long {
-    return blockIdx.x +
-           (long)__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) * gridDim.x;
+    const long t = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return claim_pos(t);
   };
   long nextp = claim();
   double ny = 0.0;
@@ -409,7 +418,7 @@ __global__ void __launch_bounds__(kBlock) ecs_group_kernel(SweepArgs a) {
     int v = 0;
     if (gl == 0) v = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     v = __shfl(v, 0, G);
-    return blockIdx.x + (long)v * gridDim.x;
+    return claim_pos(v);
   };
   long nextp = claim();
   double ny = 0.0;
