@@ -84,6 +84,15 @@ PHT_HD2 void pht_stream_init(pht_stream *s, uint32_t k0, uint32_t k1, uint32_t o
   s->b0 = s->b1 = s->b2 = s->b3 = 0u;
 }
 
+/* as pht_stream_init, with block 0 already generated (w = its four words) */
+PHT_HD2 void pht_stream_init_block0(pht_stream *s, uint32_t k0, uint32_t k1, uint32_t obs, uint32_t tag,
+                                    uint32_t sweep, pht_u32x4 w) {
+  pht_stream_init(s, k0, k1, obs, tag, sweep);
+  s->a0 = w.v[0]; s->a1 = w.v[1]; s->a2 = w.v[2]; s->a3 = w.v[3];
+  s->na = 4;
+  s->blk = 1;
+}
+
 PHT_HD2 pht_u32x4 pht_stream_block(pht_stream *s) {
   pht_u32x4 c; c.v[0] = s->obs; c.v[1] = s->tag; c.v[2] = s->sweep; c.v[3] = s->blk++;
   return pht_philox4x32_10(c, s->k0, s->k1);

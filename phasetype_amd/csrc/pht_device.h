@@ -765,6 +765,14 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
   bool haveE0;
   double lastd;
   double Elast[PHT_VEC(NT)];
+  double lammax;            /* max_i |lambda_i| (init4) */
+  double Wr[PHT_VEC(NT)];   /* W[j, .] in registers */
+  __device__ __forceinline__ void load(double lam) {
+    const int n = P.n();
+#pragma unroll
+    for (int i = 0; i < n; i++) Wr[i] = P.W(j, i);
+    lammax = lam;
+  }
   __device__ __forceinline__ double operator()(double d) {
     const int n = P.n();
     const double x = y_t - d;
@@ -775,8 +783,7 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
 #pragma unroll
       for (int i = 0; i < n; i++) Elast[i] = pht_exp_neg(P.evals(i) * x);
     }
-    const int jj = j;
-    const double acc = dev_dot16([&](int i) { return P.W(jj, i); }, Elast, n);
+    const double acc = dev_dot16([&](int i) { return Wr[i]; }, Elast, n);
     lastd = d;
     return pht_log(acc) + Sjj * d;
   }
@@ -785,11 +792,7 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
   static constexpr bool kInit4 = true;
   __device__ __forceinline__ void init4(const double xinit[4], double yv[4]) {
     const int n = P.n();
-    const int jj = j;
-    auto Wj = [&](int i) { return P.W(jj, i); };
-    double lammax = 0.0;
-#pragma unroll
-    for (int i = 0; i < n; i++) lammax = fmax(lammax, fabs(P.evals(i)));
+    auto Wj = [&](int i) { return Wr[i]; };
     const double x3 = y_t - xinit[3];
     double acc[4];
     if (pht_ecs_init_ok(lammax, xinit[0], x3)) {
@@ -828,8 +831,19 @@ struct EcsLane {
   double yt;                 /* remaining time y - t, carried as yt <- yt - d (device spec) */
   int j, njump;
   bool haveE0;               /* E0 valid for the current remaining time */
+  bool haveDen;              /* den valid for (j, E0) */
+  double den;                /* pht_dot16(QQs[j,.], E0): moveMass computed it for the chosen state */
   double E0[PHT_VEC(NT)];    /* e^{λ_i yt}: absorb test / previous moveMass */
 };
+
+/* max_i |lambda_i| of the sweep (uniform) */
+template <int NT>
+__device__ __forceinline__ double lam_max(const Par<NT> &P) {
+  double m = 0.0;
+#pragma unroll
+  for (int i = 0; i < P.n(); i++) m = fmax(m, fabs(P.evals(i)));
+  return m;
+}
 
 template <int NT, class Sink>
 __device__ __forceinline__ void ecs_begin(const Par<NT> &P, double y, Lane &ln, Sink &sk, EcsLane<NT> &st) {
@@ -840,6 +854,7 @@ __device__ __forceinline__ void ecs_begin(const Par<NT> &P, double y, Lane &ln, 
   st.j = B;
   st.njump = 0;
   st.haveE0 = false;
+  st.haveDen = false;
 }
 
 /* absorb test at the current state (LJMA_probAbsorb + runif, :251-255);
@@ -859,8 +874,9 @@ __device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink 
 #pragma unroll
       for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
       st.haveE0 = true;
+      st.haveDen = false;
     }
-    const double den = dev_dot16([&](int i) { return P.QQs(j, i); }, st.E0, n);
+    const double den = st.haveDen ? st.den : dev_dot16([&](int i) { return P.QQs(j, i); }, st.E0, n);
     const double pab = pht_exp(fma(P.S(j, j), y_t, P.logs(j)) - pht_log(den));
     fin = (U < pab);
   }
@@ -899,14 +915,14 @@ __device__ __forceinline__ void ecs_jump_finish(const Par<NT> &P, Lane &ln, Sink
   st.yt = x;
   st.haveE0 = true;
   const int cnt = P.nsuccP(j);
-  double w[PHT_VEC(NT)];
+  double w[PHT_VEC(NT)], accs[PHT_VEC(NT)];
   double sum = 0.0;
 #pragma unroll
   for (int q = 0; q < PHT_VEC(NT); q++) {
     if (q < cnt) {
       const int k = P.succP(j, q);
-      const double acc = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
-      w[q] = P.P(j, k) * acc;
+      accs[q] = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
+      w[q] = P.P(j, k) * accs[q];
       sum += w[q];
     }
   }
@@ -927,6 +943,12 @@ __device__ __forceinline__ void ecs_jump_finish(const Par<NT> &P, Lane &ln, Sink
       sel = cnt - 1;
     }
     nj = (cnt > 0) ? P.succP(j, sel) : 0;
+    /* the next absorb test's denominator: same dot product, same E */
+    double dsel = 0.0;
+#pragma unroll
+    for (int q = 0; q < PHT_VEC(NT); q++) dsel = (q == sel) ? accs[q] : dsel;
+    st.den = dsel;
+    st.haveDen = (cnt > 0);
   }
   sk.z(j, d);
   sk.N(j, nj);
@@ -936,8 +958,14 @@ __device__ __forceinline__ void ecs_jump_finish(const Par<NT> &P, Lane &ln, Sink
 }
 
 template <int NT>
+__device__ __forceinline__ EcsDens<NT> ecs_dens(const Par<NT> &P, EcsLane<NT> &st, double lam) {
+  EcsDens<NT> f{P, st.j, st.yt, P.S(st.j, st.j), st.E0, true, -1.0, {}, 0.0, {}};
+  f.load(lam);
+  return f;
+}
+template <int NT>
 __device__ __forceinline__ EcsDens<NT> ecs_dens(const Par<NT> &P, EcsLane<NT> &st) {
-  return EcsDens<NT>{P, st.j, st.yt, P.S(st.j, st.j), st.E0, true, -1.0, {}};
+  return ecs_dens(P, st, lam_max(P));
 }
 
 /* start of a non-absorbing jump: ARMS sojourn (:307-342).  With `pend`

@@ -237,18 +237,18 @@ __device__ __forceinline__ double round_metropolis(const Env &e, const WPt &p, d
  */
 template <int NT, class Env, class Sink>
 __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st, bool start,
-                                          bool &pend, ArmsPend &pd) {
+                                          bool &pend, ArmsPend &pd, double lam) {
   const int n = P.n();
   const double y_t = st.yt;
-  /* converged: the next Philox block for this round's draws (invert, test,
-   * Metropolis, moveMass: at most 4 words) */
-  if (start || pend) pht_stream_topup(&ln.r);
+  /* (the caller has generated the next Philox block for this round's
+   * draws: invert, test, Metropolis, moveMass, at most 4 words) */
   if (start && !st.haveE0) { /* s_j = 0: no absorb test ran at this state */
 #pragma unroll
     for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
     st.haveE0 = true;
+    st.haveDen = false;
   }
-  EcsDens<NT> f = ecs_dens(P, st);
+  EcsDens<NT> f = ecs_dens(P, st, lam);
   double xsamp = 0.0;
   int ainfo = 0;
   bool fin = false;  /* the jump ends this round without an iteration */

@@ -250,10 +250,37 @@ ecs_exact_kernel(SweepArgs a) {
    * step per round (ecs_jump_resume) while the other lanes go on */
   ArmsPend pd;
   bool pend = false;
+  const double lam = lam_max(P);
+  /* Philox blocks generated ahead at converged points, one per lane per
+   * point: the current stream's next block, or else block 0 of the next
+   * observation (so a new observation never runs Philox divergently) */
+  pht_u32x4 nxw;
+  bool nxReady = false;
+  auto topup = [&](bool act) {
+    const bool cur = act && have && !ln.r.nb;
+    const bool nxt = act && !cur && !nxReady && nextp < a.count;
+    if (cur || nxt) {
+      pht_u32x4 c;
+      c.v[0] = cur ? ln.r.obs : ngid;
+      c.v[1] = cur ? ln.r.tag : 0u;
+      c.v[2] = a.sweep;
+      c.v[3] = cur ? ln.r.blk : 0u;
+      const pht_u32x4 w = pht_philox4x32_10(c, a.k0, a.k1);
+      if (cur) {
+        ln.r.b0 = w.v[0]; ln.r.b1 = w.v[1]; ln.r.b2 = w.v[2]; ln.r.b3 = w.v[3];
+        ln.r.nb = 1;
+        ln.r.blk++;
+      } else {
+        nxw = w;
+        nxReady = true;
+      }
+    }
+  };
+  /* per-lane observation counters, flushed once at the end */
+  unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
   for (;;) {
     bool need = false;
-    /* converged: generate the next Philox block ahead for the absorb tests */
-    if (have && !pend) pht_stream_topup(&ln.r);
+    topup(!pend);
     while (!done && !pend) {
       if (!have) {
         if (nextp >= a.count) {
@@ -268,7 +295,9 @@ ecs_exact_kernel(SweepArgs a) {
           ny = a.y[a.begin + nextp];
           ngid = a.gid[a.begin + nextp];
         }
-        pht_stream_init(&ln.r, a.k0, a.k1, gobs, 0u, a.sweep);
+        if (nxReady) pht_stream_init_block0(&ln.r, a.k0, a.k1, gobs, 0u, a.sweep, nxw);
+        else pht_stream_init(&ln.r, a.k0, a.k1, gobs, 0u, a.sweep);
+        nxReady = false;
         ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
         if (DEBUG) {
           sk.dz = a.dbg_zq + pos * n;
@@ -285,11 +314,11 @@ ecs_exact_kernel(SweepArgs a) {
           a.dbg_flags[pos] = ln.flags;
           a.dbg_ndraw[pos] = nd;
         }
-        lds_add(&xc[0], 1ull);
-        lds_add(&xc[1], (unsigned long long)ln.neval);
-        if (ln.flags) lds_add(&xc[2], 1ull);
-        lds_add(&xc[3], (unsigned long long)nd);
-        lds_add(&xc[4], (unsigned long long)ln.njump);
+        c_obs++;
+        c_neval += ln.neval;
+        c_flag += ln.flags ? 1u : 0u;
+        c_nd += nd;
+        c_jump += ln.njump;
         have = false;
         continue;
       }
@@ -307,9 +336,15 @@ ecs_exact_kernel(SweepArgs a) {
     if (pend) pend = !ecs_jump_resume(P, ln, env, sk, st, pd);
     if (need) pend = !ecs_jump_start(P, ln, env, sk, st, &pd);
 #else
-    ecs_round(P, ln, env, sk, st, need, pend, pd);
+    topup(need || pend);
+    ecs_round(P, ln, env, sk, st, need, pend, pd, lam);
 #endif
   }
+  lds_add(&xc[0], (unsigned long long)c_obs);
+  lds_add(&xc[1], (unsigned long long)c_neval);
+  lds_add(&xc[2], (unsigned long long)c_flag);
+  lds_add(&xc[3], (unsigned long long)c_nd);
+  lds_add(&xc[4], (unsigned long long)c_jump);
 #ifdef PHT_STAMPS
   if ((threadIdx.x & 63) == 0)
     for (int q = 0; q < 8; q++) lds_add(&xc[8 + q], ln.st_acc[q]);
