@@ -18,7 +18,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(OUT_DIR, "libPhaseType.so")
 SOURCES = ["pht_kernels.hip", "gibbs_host.cpp", "rstream.c"]
-HEADERS = ["pht_device.h", "pht_env.h", "pht_kernels.h", "pht_layout.h", "rstream.h"]
+HEADERS = ["pht_device.h", "pht_env.h", "pht_kernels.h", "pht_layout.h", "rstream.h", "pht_ecs_round.h", "pht_ecs_group.h"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 DEFAULT_DEFINES: tuple = ("PHT_DETMATH_LDS", "PHT_ENV_K=9")
 

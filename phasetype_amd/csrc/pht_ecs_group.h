@@ -533,12 +533,14 @@ __device__ __forceinline__ void g_round(const Par<NT> &P, Lane &ln, GEnv &env, E
     fin = true;
   }
   bool acc = false;
+  WPt q;
+  double ynew = 0.0, yv = 0.0;
+  const bool start0 = start, big0 = big;
   if (arm && !fin) {
-    WPt q;
     ginvert(env, dev_u(ln.r), q);
     const double u = dev_u(ln.r) * q.ey;
-    const double yv = logshift(u, env.ymax);
-    const double ynew = f(q.x);
+    yv = logshift(u, env.ymax);
+    ynew = f(q.x);
     ln.neval++;
     if (yv >= ynew) {
       pd.px = q.x; pd.py = ynew; pd.pey = expshift(ynew, env.ymax); pd.pr = q.pr;
@@ -571,7 +573,8 @@ __device__ __forceinline__ void g_round(const Par<NT> &P, Lane &ln, GEnv &env, E
       const int r = i & 15, h = i >> 4;
       E0f[i] = __shfl(st.E0[h * SL::Q + r / G], r % G, G);
     }
-    EcsDens<NT> f1{P, st.j, st.yt, P.S(st.j, st.j), E0f, true, -1.0, {}};
+    EcsDens<NT> f1{P, st.j, st.yt, P.S(st.j, st.j), E0f, true, -1.0, {}, 0.0, {}};
+    f1.load(lam_max(P)); /* W[j, .] into registers (the density's weights) */
     const int rc = arms_step(benv, f1, pd, 0.0, xsamp, ln);
     if (rc != 1) {
       ainfo = rc;
@@ -591,6 +594,12 @@ __device__ __forceinline__ void g_round(const Par<NT> &P, Lane &ln, GEnv &env, E
         }
     }
   }
+#ifdef PHT_TRACE_GID
+  if (ln.r.obs == PHT_TRACE_GID && gl == 0 && (start0 || pend || big0 || acc || fin))
+    printf("T%d j=%d yt=%.17g st=%d pend=%d big=%d cnt=%d qx=%.17g ynew=%.17g yv=%.17g acc=%d xs=%.17g ai=%d\n", G,
+           st.j, y_t, (int)start0, (int)pend, (int)big0, big0 ? benv.cnt : env.cnt, q.x, ynew, yv, (int)acc, xsamp,
+           ainfo);
+#endif
   if (acc || fin) {
     pend = false;
     g_jump_finish<NT, G>(P, ln, sk, st, f, xsamp, ainfo, gl);

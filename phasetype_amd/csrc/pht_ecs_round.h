@@ -356,6 +356,11 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
     }
   }
   PHT_STAMP(ln, 2);
+#ifdef PHT_TRACE_GID
+  if (ln.r.obs == PHT_TRACE_GID && (start || pend || big || acc || fin))
+    printf("T1 j=%d yt=%.17g st=%d pend=%d big=%d cnt=%d qx=%.17g ynew=%.17g yv=%.17g acc=%d xs=%.17g ai=%d\n", st.j,
+           y_t, (int)start, (int)pend, (int)big, env.cnt, q.x, ynew, yv, (int)acc, xsamp, ainfo);
+#endif
   if (acc || fin) {
     pend = false;
     ecs_jump_finish(P, ln, sk, st, f, xsamp, ainfo);

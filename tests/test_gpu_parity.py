@@ -162,3 +162,30 @@ def test_grid_occupancy_invariance(gpu, monkeypatch, occ):
     monkeypatch.setenv("PHT_ECS_OCC", str(occ))
     got = sw.sweep(S, s, key=(1, 9), sweep=2, zexp=zexp)
     assert np.array_equal(ref[:2 * n + n * n], got[:2 * n + n * n])
+
+
+@pytest.mark.parametrize("group", [1, 2, 4, 8])
+def test_longest_paths_bitexact(gpu, orc, monkeypatch, group):
+    """The longest latent paths (the 4096 largest of 1e6 absorption times:
+    ~20-50 jumps, envelopes that outgrow the converged code and the lane
+    groups' LDS envelope) through the one-lane and the lane-group ECS
+    kernels, per observation against the oracle's device specification,
+    for three (key, sweep) pairs."""
+    monkeypatch.setenv("PHT_GROUP", str(group))
+    n = 10
+    S0, s0 = bd_exit(n)
+    y, cen = simulate_ph(S0, s0, 1_000_000, seed=4242)
+    idx = np.sort(np.argsort(-y)[:4096])
+    y, cen = np.ascontiguousarray(y[idx]), np.ascontiguousarray(cen[idx])
+    zexp = int(orc.lib.orc_zexp(np.ascontiguousarray(y), len(y)))
+    sw = P.Sweeper(n, 2, 1)
+    sw.set_obs(y, cen)
+    for key, sweep in (((5, 6), 2), ((3, 4), 1), ((9, 1), 7)):
+        o = orc.dev_sweep(2, S0, s0, y, cen, key=key, sweep=sweep, zexp=zexp)
+        g = sw.sweep_debug(S0, s0, key=key, sweep=sweep, zexp=zexp)
+        bad = np.nonzero((g["ndraw"] != o["ndraw"]) | np.any(g["zq"] != o["zq"], axis=1))[0]
+        assert len(bad) == 0, (f"{len(bad)} observations differ, first {bad[:5]}: ndraw gpu "
+                               f"{g['ndraw'][bad[:5]]} oracle {o['ndraw'][bad[:5]]} flags {g['flags'][bad[:5]]}")
+        for f in ("B", "pre", "flags"):
+            assert np.array_equal(g[f], o[f]), f
+        assert np.array_equal(g["N"], o["N"])

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Kernel time of the ECS-exact sweep against the shard size (strong-scaling
+regime) for the launch variants the host can pick at run time:
+PHT_GROUP (lanes per observation) and PHT_ECS_OCC (blocks per CU).
+
+usage (GPU box): python3 tools/latency.py [--Ns 62500 125000 ...] [--sweeps 8]
+Shard = the first N observations of the bench data set (what rank 0 of
+1e6/N GPUs holds).  "topK" entries use the K largest observations instead
+(one lone wavefront for K=64: the per-round latency of the longest paths).
+Every variant must reproduce the first variant's draws (identical results).
+Prints one JSON object per shard size.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import phasetype_amd as P  # noqa: E402
+from phasetype_amd.synth import DATA_KEY, bd_exit, bd_exit_structure, simulate_ph  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=10)
+    ap.add_argument("--Ns", nargs="+", default=["top64", "top4096", "31250", "62500", "125000", "250000"])
+    ap.add_argument("--variants", nargs="+", default=["g1o2", "g1o1", "g2", "g4", "g8"])
+    ap.add_argument("--sweeps", type=int, default=8)
+    a = ap.parse_args()
+    n = a.n
+    S, s = bd_exit(n)
+    T, theta = bd_exit_structure(n)
+    nu, zeta = 1 + 50 * theta, np.full(len(theta), 50.0)
+    y, cen = simulate_ph(S, s, 1_000_000, seed=DATA_KEY, censor_frac=0.0)
+    zexp = P.zexp_for(y)
+    Cm = np.ones(T.shape)
+    for spec in a.Ns:
+        if spec.startswith("top"):
+            k = int(spec[3:])
+            idx = np.sort(np.argsort(-y)[:k])
+        else:
+            idx = np.arange(int(spec))
+        ys, cs = np.ascontiguousarray(y[idx]), np.ascontiguousarray(cen[idx])
+        sw = P.Sweeper(n, 2, 1, device=0)
+        sw.set_obs(ys, cs, obs0=0)
+        out = {"N": spec}
+        ref = None
+        for v in a.variants:
+            os.environ.pop("PHT_GROUP", None)
+            os.environ.pop("PHT_ECS_OCC", None)
+            if v.startswith("g1o"):
+                os.environ["PHT_GROUP"] = "1"
+                os.environ["PHT_ECS_OCC"] = v[3:]
+            else:
+                os.environ["PHT_GROUP"] = v[1:]
+            P.set_seed(5)
+            sw.gibbs(2, 2, nu, zeta, T, Cm, zexp)  # warm-up
+            P.set_seed(7)
+            sw.kernel_ms_total = 0.0
+            t0 = time.perf_counter()
+            res = sw.gibbs(a.sweeps + 1, 2, nu, zeta, T, Cm, zexp)
+            dt = time.perf_counter() - t0
+            same = True
+            if ref is None:
+                ref = res
+            else:
+                same = bool(np.array_equal(ref, res))
+            out[v] = {"kernel_ms": round(sw.kernel_ms_total / a.sweeps, 4),
+                      "sweep_ms": round(dt / a.sweeps * 1e3, 4), "same": same}
+        sw.close()
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

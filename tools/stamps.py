@@ -16,9 +16,14 @@ from phasetype_amd.synth import DATA_KEY, bd_exit, simulate_ph  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=10)
 ap.add_argument("--N", type=int, default=1_000_000)
+ap.add_argument("--top", type=int, default=0, help="only the TOP largest observations (lone-wave latency)")
 a = ap.parse_args()
 S, s = bd_exit(a.n)
 y, cen = simulate_ph(S, s, a.N, seed=DATA_KEY)
+if a.top:
+    idx = np.sort(np.argsort(-y)[:a.top])
+    y, cen = np.ascontiguousarray(y[idx]), np.ascontiguousarray(cen[idx])
+    a.N = a.top
 sw = P.Sweeper(a.n, 2)
 sw.set_obs(y, cen)
 zexp = P.zexp_for(y)
