@@ -98,12 +98,22 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # backend "nccl" = RCCL over xGMI (one GPU per rank).  PHT_DIST_BACKEND=gloo
+    # rehearses the multi-rank flow on a box with fewer GPUs than ranks (ranks
+    # share devices round-robin, the statistics travel through host memory).
+    backend = os.environ.get("PHT_DIST_BACKEND", "nccl")
+    coll_dev = "cpu"
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            coll_dev = f"cuda:{local}"
+        else:
+            dist.init_process_group(backend)
+            local = local % max(1, P.device_count())
 
     n, N = args.n, args.N
     method = P.METHODS[args.method]
@@ -120,14 +130,15 @@ def main():
 
     reduce = None
     if dist is not None:
-        reduce = make_stats_allreduce(dist, P.stats_len(n), device=f"cuda:{local}")
+        reduce = make_stats_allreduce(dist, P.stats_len(n), device=coll_dev)
 
     def sync():
         if dist is not None:
             import torch
 
             dist.barrier()
-            torch.cuda.synchronize()
+            if coll_dev != "cpu":
+                torch.cuda.synchronize()
 
     P.set_seed(20241008)
     warm = sw.gibbs(args.warmup + 1, method, nu, zeta, T, Cm, zexp, reduce=reduce)
@@ -139,7 +150,7 @@ def main():
     dt = time.perf_counter() - t0
     kernel_ms = sw.kernel_ms_total / args.steps
     if dist is not None:
-        dt, kernel_ms = max_over_ranks(dist, [dt, kernel_ms], device=f"cuda:{local}")
+        dt, kernel_ms = max_over_ranks(dist, [dt, kernel_ms], device=coll_dev)
     if not np.all(np.isfinite(res)):
         raise SystemExit("non-finite Gibbs draws")
 

@@ -198,7 +198,14 @@ static int eigen(int n, const double *S, double *evals, double *Q, double *Qinv)
   if ((int)wq > lw) lw = (int)wq;
   std::vector<double> work(lw > 0 ? lw : 1);
   memcpy(A.data(), S, sizeof(double) * n * n);
-  p_dgeevx(&balanc, &jobv, &jobv, &sense, &nn, A.data(), &nn, evals, evi.data(), Ql.data(), &nn, Q, &nn, &ilo,
+  /* The reference asks for condition numbers too (sense 'B'); they come
+   * from dtrsna AFTER the eigenvectors and feed nothing it uses, so the
+   * sweep skips them (sense 'N', same workspace as the 'B' query: the
+   * Hessenberg/Schur/eigenvector arithmetic is unchanged — evals, Q and
+   * Q^-1 stay bit-identical, tests/test_host.py).  That is most of the
+   * per-sweep host time at n = 10. */
+  char sense_n = 'N', jobvl_n = 'N';
+  p_dgeevx(&balanc, &jobvl_n, &jobv, &sense_n, &nn, A.data(), &nn, evals, evi.data(), Ql.data(), &nn, Q, &nn, &ilo,
            &ihi, scl.data(), &abnrm, rce.data(), rcv.data(), work.data(), &lw, iwork.data(), &info, 1, 1, 1, 1);
   if (info != 0) {
     say("Error (LJMA_eigen 01): failed LAPACK call, code=%d\n", info);
@@ -263,15 +270,17 @@ static int build_params(int n, const double *S, const double *s, int method, std
       }
     }
   }
+  std::vector<double> rj(n);
   for (int j = 0; j < n; j++) {
     const double Sjj = S[j + j * n];
     d[L.logs + j] = s[j] > 0.0 ? pht_log(s[j]) : 0.0;
     d[L.scale + j] = 1.0 / -Sjj;
     d[L.logscale + j] = pht_log(d[L.scale + j]);
+    for (int k = 0; k < n; k++) rj[k] = S[j + k * n] / (-Sjj); /* hoisted: same quotients */
     for (int i = 0; i < n; i++) {
       double w = 0.0, v = 0.0;
       for (int k = 0; k < n; k++) {
-        if (k != j) w = fma(S[j + k * n] / (-Sjj), Q[k + i * n], w);
+        if (k != j) w = fma(rj[k], Q[k + i * n], w);
         v = fma(P[j + k * n], Q[k + i * n], v);
       }
       d[L.QQs + j + i * n] = Q[j + i * n] * Qs[i];
@@ -329,6 +338,9 @@ struct pht_ctx {
   double *d_y = nullptr;
   int *d_cens = nullptr;
   uint32_t *d_gid = nullptr;
+  /* MHRS attempt-search workspace (count * (1 + mhit) tasks) */
+  uint32_t *d_mbest = nullptr, *d_mq0 = nullptr, *d_mq1 = nullptr;
+  unsigned *d_mcnt = nullptr;
   unsigned char *d_params = nullptr;
   unsigned long long *d_stats = nullptr;
   unsigned long long *h_stats = nullptr; /* pinned */
@@ -348,7 +360,13 @@ static void ctx_free_obs(pht_ctx *c) {
   if (c->d_y) (void)hipFree(c->d_y);
   if (c->d_cens) (void)hipFree(c->d_cens);
   if (c->d_gid) (void)hipFree(c->d_gid);
+  if (c->d_mbest) (void)hipFree(c->d_mbest);
+  if (c->d_mq0) (void)hipFree(c->d_mq0);
+  if (c->d_mq1) (void)hipFree(c->d_mq1);
+  if (c->d_mcnt) (void)hipFree(c->d_mcnt);
   c->d_y = nullptr; c->d_cens = nullptr; c->d_gid = nullptr;
+  c->d_mbest = c->d_mq0 = c->d_mq1 = nullptr;
+  c->d_mcnt = nullptr;
 }
 static void ctx_free_dbg(pht_ctx *c) {
   (void)hipSetDevice(c->device);
@@ -381,6 +399,10 @@ extern "C" pht_ctx *pht_ctx_create(int device, int n, int method, int mhit) {
   }
   if (device < 0 || device >= ndev) {
     set_err("device %d out of range (%d devices)", device, ndev);
+    return nullptr;
+  }
+  if (dispatch_method(method) == kMethodMHRS && (mhit < 0 || mhit > 1022)) {
+    set_err("mhit=%d outside 0..1022 (MHRS attempt streams carry the chain index in 10 bits)", mhit);
     return nullptr;
   }
   pht_ctx *c = new pht_ctx();
@@ -459,6 +481,13 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
   HIPCHK(hipMemcpy(c->d_y, ys.data(), sizeof(double) * count, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(c->d_cens, cs.data(), sizeof(int) * count, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(c->d_gid, gs.data(), sizeof(uint32_t) * count, hipMemcpyHostToDevice));
+  if (c->method == kMethodMHRS) {
+    const size_t tasks = (size_t)count * (size_t)(1 + c->mhit);
+    HIPCHK(hipMalloc(&c->d_mbest, sizeof(uint32_t) * tasks));
+    HIPCHK(hipMalloc(&c->d_mq0, sizeof(uint32_t) * tasks));
+    HIPCHK(hipMalloc(&c->d_mq1, sizeof(uint32_t) * tasks));
+    HIPCHK(hipMalloc(&c->d_mcnt, sizeof(unsigned) * kMhrsCounters));
+  }
   return 0;
 }
 
@@ -501,6 +530,10 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   a.sweep = sweep;
   a.zscale = ldexp(1.0, zexp);
   a.stats = c->d_stats;
+  a.mbest = c->d_mbest;
+  a.mq0 = c->d_mq0;
+  a.mq1 = c->d_mq1;
+  a.mcnt = c->d_mcnt;
   if (debug) {
     if (c->dbg_cap < c->count) {
       ctx_free_dbg(c);

@@ -9,8 +9,9 @@
  *                  (+ LJMA_probAbsorb :120-136, LJMA_ECS_dens :150-171, LJMA_moveMass :21-41)
  *   censored       LJMA_samplechain / LJMA_condjump_r_ars / LJMA_condjumpdens
  *                  src/Simulate_AbsCTMC_gt_Aslett_DCS.c:111-418
- *   mhrs           LJMA_MHsample_Bladt + LJMA_samplechain_Bladt
- *                  src/Simulate_AbsCTMC_eq_Bladt_MHRS.c:37-117, src/Simulate_AbsCTMC_gt_Bladt_MHRS.c:151-277
+ *   mhrs_attempt   one attempt of LJMA_samplechain_Bladt (the search over
+ *                  attempts and LJMA_MHsample_Bladt's MH step: pht_mhrs.h)
+ *                  src/Simulate_AbsCTMC_eq_Bladt_MHRS.c:37-117, src/Simulate_AbsCTMC_gt_Bladt_MHRS.c:34-160
  *   dcs            LJMA_Hobolth_endState + LJMA_samplechain_Hobolth + HobCDF + Find02
  *                  src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:11-51, src/Simulate_AbsCTMC_gt_Hobolth_DCS.c:23-226,
  *                  src/utility.c:233-338
@@ -139,7 +140,7 @@ struct Lane {
   int nbrent;
   int njump;
 #ifdef PHT_STAMPS
-  unsigned long long st_last, st_acc[8], st_rounds;
+  unsigned long long st_last, st_acc[15], st_rounds;
 #endif
 };
 
@@ -1148,77 +1149,55 @@ __device__ __forceinline__ void censored(const Par<NT> &P, double y, Lane &ln, E
 }
 
 /* ================================================================ MHRS */
-/* One LJMA_samplechain_Bladt call: returns pre; pos = stream position of
- * the accepted attempt (replayed later for the statistics). */
-template <int NT>
-__device__ __forceinline__ int bladt_chain(const Par<NT> &P, double y, int cens, Lane &ln, uint32_t &pos) {
-  const int n = P.n();
-  double t = 0.0;
-  int lastj = 0, natt = 0;
-  while (t < y) {
-    if (natt++ >= kMhrsMaxAtt) {
-      ln.flags |= kFlagMhrsCap;
-      break;
-    }
-    pos = pht_stream_pos(&ln.r);
-    t = 0;
-    double target = dev_u(ln.r), sofar = 0.0;
-    int B2 = 0;
-    while (sofar < target && B2 <= n) sofar += (B2 < n ? P.pi(B2) : 0.0), B2++;
-    B2--;
-    int j = B2;
-    lastj = j;
-    int njump = 0;
-    while ((t < y && j < n) || (cens && j < n)) {
-      if (njump++ >= kMaxJumps) {
-        ln.flags |= kFlagJumpCap;
-        t = y;
-        break;
-      }
-      t = t + dev_rexp(ln.r, 1.0 / -P.S(j, j));
-      target = dev_u(ln.r);
-      const int cnt = P.nsuccPf(j);
-      sofar = 0.0;
-      int sel = n + 1;
-      for (int q = 0; q < cnt; q++) {
-        const int k = P.succPf(j, q);
-        sofar += P.Pf(j, k);
-        if (!(sofar < target)) {
-          sel = k;
-          break;
-        }
-      }
-      j = sel;
-      if ((t < y && j < n) || (cens && j < n)) lastj = j;
-    }
-  }
-  return lastj;
+/*
+ * Device specification of LJMA_MHsample_Bladt / LJMA_samplechain_Bladt
+ * (src/Simulate_AbsCTMC_eq_Bladt_MHRS.c:63-114,
+ * src/Simulate_AbsCTMC_gt_Bladt_MHRS.c:49-121).  The reference's rejection
+ * loop is a search for the FIRST successful attempt of each chain (c = 0:
+ * the current path, c = 1..mhit: the proposals).  Attempt a of chain c
+ * draws from its own Philox stream, tag ((c + 1) << 22) | a, so attempts
+ * are independent: any lanes may try them in any order (pht_mhrs.h) and the
+ * first success is the same.  An attempt succeeds when the reference
+ * accepts it (alive at y for an exact observation, absorbed after y for a
+ * censored one) and s[pre] > 0 (the caller's re-draw loop, :65-76).  The
+ * observation's own stream (tag 0) gives the mhit acceptance uniforms; the
+ * accepted chain's first successful attempt is replayed for the statistics.
+ */
+constexpr int kMhrsTagShift = 22; /* attempts per chain < 2^22 = kMhrsMaxAtt */
+__device__ __forceinline__ uint32_t mhrs_tag(int c, uint32_t att) {
+  return ((uint32_t)(c + 1) << kMhrsTagShift) | att;
 }
+constexpr uint32_t kMhrsUnresolved = 0xffffffffu;
+/* first-success record of a chain: (attempt << 8) | pre; min = first */
+__device__ __forceinline__ uint32_t mhrs_pack(uint32_t att, int pre) { return (att << 8) | (uint32_t)pre; }
 
-template <int NT, class Sink>
-__device__ __forceinline__ void bladt_replay(const Par<NT> &P, double y, int cens, Lane &ln, uint32_t pos, Sink &sk) {
+struct NoSink {
+  __device__ __forceinline__ void start(int) {}
+  __device__ __forceinline__ void z(int, double) {}
+  __device__ __forceinline__ void N(int, int) {}
+  __device__ __forceinline__ void pre(int) {}
+};
+
+/* One attempt of LJMA_samplechain_Bladt's loop (:54-121) on stream r;
+ * REC: also record the path's statistics (the accepted attempt). */
+template <int NT, bool REC, class Sink>
+__device__ __forceinline__ bool mhrs_attempt(const Par<NT> &P, double y, int cens, pht_stream &r, int &pre,
+                                             int &flags, int &njump, Sink &sk) {
   const int n = P.n();
-  pht_stream r = ln.r;
-  pht_stream_seek(&r, pos);
   double t = 0.0, lastt = 0.0, sofar = 0.0;
   double target = pht_next_u(&r);
   int B2 = 0;
   while (sofar < target && B2 <= n) sofar += (B2 < n ? P.pi(B2) : 0.0), B2++;
   B2--;
-  int j = B2, lastj = j, njump = 0;
-  sk.start(B2);
+  int j = B2, lastj = j, nj = 0;
+  if (REC) sk.start(B2);
   while ((t < y && j < n) || (cens && j < n)) {
-    if (njump++ >= kMaxJumps) {
+    if (nj++ >= kMaxJumps) {
+      flags |= kFlagJumpCap;
       t = y;
       break;
     }
-    {
-      const double sc = 1.0 / -P.S(j, j);
-      double e;
-      if (!isfinite(sc) || sc <= 0.0) e = (sc == 0.0) ? 0.0 : __builtin_nan("");
-      else e = sc * -pht_log(pht_next_u53(&r));
-      t = t + e;
-    }
+    t = t + dev_rexp(r, 1.0 / -P.S(j, j));
     target = pht_next_u(&r);
     const int cnt = P.nsuccPf(j);
     sofar = 0.0;
@@ -1233,35 +1212,32 @@ __device__ __forceinline__ void bladt_replay(const Par<NT> &P, double y, int cen
     }
     j = sel;
     if ((t < y && j < n) || (cens && j < n)) {
-      sk.z(lastj, t - lastt);
-      sk.N(lastj, j);
+      if (REC) {
+        sk.z(lastj, t - lastt);
+        sk.N(lastj, j);
+        njump++;
+      }
       lastj = j;
       lastt = t;
-      ln.njump++;
     }
   }
-  sk.z(lastj, cens ? t - lastt : y - lastt);
-  sk.N(lastj, lastj);
+  if (REC) {
+    sk.z(lastj, cens ? t - lastt : y - lastt);
+    sk.N(lastj, lastj);
+  }
+  pre = lastj;
+  return !(t < y) && lastj < n && P.s(lastj) > 0.0;
 }
 
-template <int NT, class Sink>
-__device__ __forceinline__ void mhrs(const Par<NT> &P, double y, int cens, int mhit, Lane &ln, Sink &sk) {
-  uint32_t cpos = 0, ppos = 0;
-  int cpre = bladt_chain(P, y, cens, ln, cpos);
-  while (P.s(cpre) == 0) cpre = bladt_chain(P, y, cens, ln, cpos);
-  if (cens == 0) {
-    for (int k = 0; k < mhit; k++) {
-      int ppre = bladt_chain(P, y, cens, ln, ppos);
-      while (P.s(ppre) == 0) ppre = bladt_chain(P, y, cens, ln, ppos);
-      const double U = dev_u(ln.r);
-      if (U < P.s(ppre) / P.s(cpre)) {
-        cpre = ppre;
-        cpos = ppos;
-      }
-    }
-  }
-  bladt_replay(P, y, cens, ln, cpos, sk);
-  sk.pre(cpre);
+/* attempt (c, att) of observation gid, no recording */
+template <int NT>
+__device__ __forceinline__ bool mhrs_try(const Par<NT> &P, double y, int cens, uint32_t k0, uint32_t k1,
+                                         uint32_t gid, uint32_t sweep, int c, uint32_t att, int &pre) {
+  pht_stream r;
+  pht_stream_init(&r, k0, k1, gid, mhrs_tag(c, att), sweep);
+  int fl = 0, nj = 0;
+  NoSink ns;
+  return mhrs_attempt<NT, false>(P, y, cens, r, pre, fl, nj, ns);
 }
 
 /* ================================================================= DCS */

@@ -249,6 +249,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
     st.haveDen = false;
   }
   EcsDens<NT> f = ecs_dens(P, st, lam);
+  PHT_STAMP(ln, 1);
   double xsamp = 0.0;
   int ainfo = 0;
   bool fin = false;  /* the jump ends this round without an iteration */
@@ -281,6 +282,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
       env.sX(8, y_t);
     }
   }
+  PHT_STAMP(ln, 2);
   /* ---- pending lanes: the update that ends the rejected iteration */
   if (pend) big = (env.cnt + 2 > kRoundCap);
   if (__any(pend && !big && env.cnt > 9)) {
@@ -288,25 +290,24 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
   } else {
     if (pend && !big) round_insert<11>(env, pd, f, ln);
   }
-  PHT_STAMP(ln, 1);
+  PHT_STAMP(ln, 3);
   /* ---- converged: intersections and areas over the widest envelope in
    * the wavefront (9, 11 or 13 points) */
   const bool arm = (start && !fin) || (pend && !big);
   const int cap = __any(arm && env.cnt > 11) ? 13 : (__any(arm && env.cnt > 9) ? 11 : 9);
   double cs[kRoundCap]; /* cumulative areas, cumulate -> invert */
   if (arm) {
-    if (cap == 9) {
-      round_meets<9>(env, env.cnt - 1);
-      round_cumulate<9>(env, cs);
-    } else if (cap == 11) {
-      round_meets<11>(env, env.cnt - 1);
-      round_cumulate<11>(env, cs);
-    } else {
-      round_meets<13>(env, env.cnt - 1);
-      round_cumulate<13>(env, cs);
-    }
+    if (cap == 9) round_meets<9>(env, env.cnt - 1);
+    else if (cap == 11) round_meets<11>(env, env.cnt - 1);
+    else round_meets<13>(env, env.cnt - 1);
   }
   PHT_STAMP(ln, 4);
+  if (arm) {
+    if (cap == 9) round_cumulate<9>(env, cs);
+    else if (cap == 11) round_cumulate<11>(env, cs);
+    else round_cumulate<13>(env, cs);
+  }
+  PHT_STAMP(ln, 5);
   if (start && !fin) {
     pd.yprev = f(0.0); /* xprev = 0 lies in [xl, xr] = [0, y_t] */
     ln.neval++;
@@ -317,7 +318,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
     ainfo = 4;
     fin = true;
   }
-  PHT_STAMP(ln, 5);
+  PHT_STAMP(ln, 6);
   /* ---- converged: one iteration (sample, evaluate, test) */
   bool acc = false;
   const bool itr = arm && !fin;
@@ -331,12 +332,12 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
     const double u = dev_u(ln.r) * q.ey;
     yv = logshift(u, env.ymax);
   }
-  PHT_STAMP(ln, 6);
+  PHT_STAMP(ln, 7);
   if (itr) {
     ynew = f(q.x);
     ln.neval++;
   }
-  PHT_STAMP(ln, 7);
+  PHT_STAMP(ln, 8);
   if (itr) {
     if (yv >= ynew) {
       pd.px = q.x; pd.py = ynew; pd.pey = expshift(ynew, env.ymax); pd.pr = q.pr;
@@ -347,6 +348,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
       acc = true;
     }
   }
+  PHT_STAMP(ln, 9);
   /* ---- rare: envelopes beyond kRoundCap continue in the general code */
   if (big) {
     const int rc = arms_step(env, f, pd, 0.0, xsamp, ln);
@@ -355,7 +357,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
       acc = true;
     }
   }
-  PHT_STAMP(ln, 2);
+  PHT_STAMP(ln, 10);
 #ifdef PHT_TRACE_GID
   if (ln.r.obs == PHT_TRACE_GID && (start || pend || big || acc || fin))
     printf("T1 j=%d yt=%.17g st=%d pend=%d big=%d cnt=%d qx=%.17g ynew=%.17g yv=%.17g acc=%d xs=%.17g ai=%d\n", st.j,
@@ -365,7 +367,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
     pend = false;
     ecs_jump_finish(P, ln, sk, st, f, xsamp, ainfo);
   }
-  PHT_STAMP(ln, 3);
+  PHT_STAMP(ln, 11);
 }
 
 }  // namespace pht

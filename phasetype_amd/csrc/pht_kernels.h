@@ -14,6 +14,7 @@ constexpr int kBlock = 256;
 constexpr int kMethodMHRS = 0x1;
 constexpr int kMethodECS = 0x2;
 constexpr int kMethodDCS = 0x4;
+constexpr int kMhrsCounters = 16;
 
 struct SweepArgs {
   const unsigned char *params; /* packed block (pht_layout.h), device */
@@ -29,6 +30,12 @@ struct SweepArgs {
   unsigned long long *stats;   /* [stats_len(n)] int64, accumulated */
   int group;                   /* ECS exact: lanes per observation (0/1 = one lane; 2, 4, 8) */
   int occ;                     /* ECS exact: blocks per CU of the persistent grid (0 = occupancy limit) */
+  /* MHRS attempt search (pht_kernels.hip, MHRS section): per chain task
+   * (position * (1 + mhit) + c) its first success (attempt << 8 | pre), two
+   * task queues and the queue counters; allocated by the host for MHRS */
+  uint32_t *mbest;             /* [count * (1 + mhit)] */
+  uint32_t *mq0, *mq1;         /* [count * (1 + mhit)] */
+  unsigned *mcnt;              /* [kMhrsCounters] */
   /* debug per-observation outputs (DEBUG kernels only) */
   long long *dbg_zq;           /* [count*n] */
   int *dbg_N;                  /* [count*n*n] */

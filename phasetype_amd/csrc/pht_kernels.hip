@@ -71,6 +71,202 @@ __device__ __forceinline__ long claim_pos(long t) {
   return ((t / kClaimChunk) * (long)gridDim.x + blockIdx.x) * kClaimChunk + (t % kClaimChunk);
 }
 
+/* ================================================================ MHRS */
+/*
+ * The attempt search (device spec: pht_device.h, mhrs_attempt).  Every
+ * chain of every observation is a task, task = position * (1 + mhit) + c
+ * (c = 0 the current path, 1..mhit the proposals; censored observations
+ * have only c = 0).  The first successful attempt index of a task is found
+ * in rounds of growing width, because an observation whose survival
+ * probability is p needs ~1/p attempts and p is ~uniform over the data
+ * (a few tasks per sweep need ~1e5-1e6 attempts, the reference's whole
+ * run time; one lane per observation would serialise them):
+ *   round 0  one lane per task, attempts [0, 16)             (mhrs_round0)
+ *   round r  W lanes per unresolved task, 16-32 steps of W attempts
+ *            (W = 8, 64: one wavefront segment per task, ballot per step;
+ *             W = 1024, 16384, 131072: atomicMin on the task's record, early
+ *             exit once it is below the lane's next attempt)
+ * Attempt streams are per (task, attempt), so the first success does not
+ * depend on which lane tried what.  mhrs_finish then makes the MH decisions
+ * (tag-0 stream) and replays the accepted attempt for the statistics.
+ */
+constexpr int kMhrsK0 = 16;
+struct MhrsRound {
+  int W, K;
+  uint32_t A0;
+};
+constexpr MhrsRound kMhrsRounds[5] = {
+    {8, 16, 16}, {64, 16, 144}, {1024, 16, 1168}, {16384, 16, 17552}, {131072, 32, 279696}};
+
+template <int NT>
+__device__ __forceinline__ Par<NT> stage_params(const SweepArgs &a, PHT_LDS unsigned char *lsm) {
+  const int n = nval<NT>(a.n);
+  const Layout L = make_layout(n);
+  const unsigned long long *src = reinterpret_cast<const unsigned long long *>(a.params);
+  PHT_LDS unsigned long long *dst = (PHT_LDS unsigned long long *)lsm;
+  for (int k = threadIdx.x; k < L.bytes() / 8; k += blockDim.x) dst[k] = src[k];
+  Par<NT> P;
+  P.d = (const PHT_LDS double *)lsm;
+  P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
+  P.Lr = L;
+  return P;
+}
+
+/* round 0: one lane per task; unresolved tasks -> mq0 (count mcnt[0]) */
+template <int NT>
+__global__ void __launch_bounds__(kBlock) mhrs_round0(SweepArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const Par<NT> P = stage_params<NT>(a, (PHT_LDS unsigned char *)smem);
+  pht_stage_math_tables();
+  __syncthreads();
+  const int T1 = 1 + a.mhit;
+  const long task = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (task >= a.count * T1) return;
+  const long pos = task / T1;
+  const int c = (int)(task % T1);
+  const int cens = a.cens[pos];
+  if (c > 0 && cens) { /* censored observations have no proposals */
+    a.mbest[task] = 0u;
+    return;
+  }
+  const double y = a.y[pos];
+  const uint32_t gid = a.gid[pos];
+  for (uint32_t att = 0; att < (uint32_t)kMhrsK0; att++) {
+    int pre = 0;
+    if (mhrs_try<NT>(P, y, cens, a.k0, a.k1, gid, a.sweep, c, att, pre)) {
+      a.mbest[task] = mhrs_pack(att, pre);
+      return;
+    }
+  }
+  a.mbest[task] = kMhrsUnresolved;
+  a.mq0[atomicAdd(&a.mcnt[0], 1u)] = (uint32_t)task;
+}
+
+/* round with W lanes per task over the tasks in qin[0 .. *cin); W <= 64:
+ * unresolved tasks are appended to qout (count *cout) */
+template <int NT, int W, int K>
+__global__ void __launch_bounds__(kBlock) mhrs_round(SweepArgs a, uint32_t A0, const uint32_t *qin,
+                                                     const unsigned *cin, uint32_t *qout, unsigned *cout) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const Par<NT> P = stage_params<NT>(a, (PHT_LDS unsigned char *)smem);
+  pht_stage_math_tables();
+  __syncthreads();
+  const int T1 = 1 + a.mhit;
+  const long total = (long)(*cin) * W;
+  const int lane = threadIdx.x & 63;
+  const long gsize = (long)gridDim.x * kBlock;
+  /* wave-uniform loop: a wavefront holds 64 consecutive items (W | 64 keeps
+   * a task's lanes in one wavefront segment) */
+  for (long b = (long)blockIdx.x * kBlock + (threadIdx.x & ~63); b < total; b += gsize) {
+    const long item = b + lane;
+    const bool live = item < total;
+    uint32_t task = 0;
+    int c = 0, cens = 0, l = 0;
+    double y = 0.0;
+    uint32_t gid = 0;
+    if (live) {
+      task = qin[item / W];
+      l = (int)(item % W);
+      const long pos = task / T1;
+      c = (int)(task % T1);
+      y = a.y[pos];
+      cens = a.cens[pos];
+      gid = a.gid[pos];
+    }
+    bool act = live, found = false;
+    const int seg0 = (W >= 64) ? 0 : (lane & ~(W - 1));
+    for (int k = 0; k < K; k++) {
+      const uint32_t att = A0 + (uint32_t)l + (uint32_t)W * (uint32_t)k;
+      if (att >= (uint32_t)kMhrsMaxAtt) act = false;
+      if constexpr (W > 64) {
+        if (act) {
+          const uint32_t cur = __hip_atomic_load(&a.mbest[task], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((cur >> 8) < att) act = false;
+        }
+        if (!__any(act)) break;
+      }
+      int pre = 0;
+      const bool ok = act && mhrs_try<NT>(P, y, cens, a.k0, a.k1, gid, a.sweep, c, att, pre);
+      if constexpr (W <= 64) {
+        const unsigned long long m = __ballot(ok);
+        const unsigned long long segm = (W >= 64) ? ~0ull : (((1ull << W) - 1ull) << seg0);
+        const unsigned long long sm = m & segm;
+        const int first = sm ? (__ffsll((long long)sm) - 1) : lane;
+        const int fpre = __shfl(pre, first);
+        if (sm) {
+          if (live && lane == seg0 && !found)
+            a.mbest[task] = mhrs_pack(A0 + (uint32_t)(first - seg0) + (uint32_t)W * (uint32_t)k, fpre);
+          found = true;
+          act = false;
+        }
+        if (!__any(act)) break;
+      } else {
+        if (ok) {
+          atomicMin(&a.mbest[task], mhrs_pack(att, pre));
+          act = false;
+        }
+      }
+    }
+    if constexpr (W <= 64) {
+      if (live && lane == seg0 && !found) qout[atomicAdd(cout, 1u)] = task;
+    }
+  }
+}
+
+/* tasks of qin still unresolved -> qout */
+__global__ void __launch_bounds__(kBlock) mhrs_compact(SweepArgs a, const uint32_t *qin, const unsigned *cin,
+                                                       uint32_t *qout, unsigned *cout) {
+  const long cnt = *cin;
+  for (long q = (long)blockIdx.x * kBlock + threadIdx.x; q < cnt; q += (long)gridDim.x * kBlock) {
+    const uint32_t task = qin[q];
+    if (a.mbest[task] == kMhrsUnresolved) qout[atomicAdd(cout, 1u)] = task;
+  }
+}
+
+/* LJMA_MHsample_Bladt's MH step over the chains' first successes, then the
+ * accepted attempt replayed with recording.  ln.neval <- attempts made. */
+template <int NT, class Sink>
+__device__ __forceinline__ void mhrs_finish(const Par<NT> &P, const SweepArgs &a, long i, double y, int cens,
+                                            Lane &ln, Sink &sk) {
+  const int T1 = 1 + a.mhit;
+  const uint32_t gid = a.gid[i];
+  auto first = [&](int c, int &pre) -> uint32_t {
+    const uint32_t b = a.mbest[i * T1 + c];
+    if (b != kMhrsUnresolved) {
+      pre = (int)(b & 0xffu);
+      return b >> 8;
+    }
+    /* no success within the cap: the last attempt, flagged */
+    ln.flags |= kFlagMhrsCap;
+    const uint32_t att = (uint32_t)kMhrsMaxAtt - 1u;
+    (void)mhrs_try<NT>(P, y, cens, a.k0, a.k1, gid, a.sweep, c, att, pre);
+    return att;
+  };
+  int cpre = 0;
+  uint32_t catt = first(0, cpre);
+  uint32_t natt = catt + 1u;
+  int cc = 0;
+  if (cens == 0) {
+    for (int k = 1; k <= a.mhit; k++) {
+      int ppre = 0;
+      const uint32_t patt = first(k, ppre);
+      natt += patt + 1u;
+      const double U = dev_u(ln.r);
+      if (U < P.s(ppre) / P.s(cpre)) {
+        cpre = ppre;
+        catt = patt;
+        cc = k;
+      }
+    }
+  }
+  pht_stream r;
+  pht_stream_init(&r, a.k0, a.k1, gid, mhrs_tag(cc, catt), a.sweep);
+  int pre2 = 0;
+  (void)mhrs_attempt<NT, true>(P, y, cens, r, pre2, ln.flags, ln.njump, sk);
+  sk.pre(cpre);
+  ln.neval = (int)natt;
+}
+
 template <int NT, int METHOD, bool DEBUG, class Env>
 __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -113,14 +309,15 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
     const double y = a.y[i];
     Env env;
     if (METHOD == kMethodMHRS) {
-      mhrs<NT>(P, y, a.cens[i], a.mhit, ln, sk);
+      mhrs_finish<NT>(P, a, i, y, a.cens[i], ln, sk);
     } else if (METHOD == kMethodDCS) {
       dcs<NT>(P, y, ln, sk);
     } else {
       if (a.cens[i]) censored<NT>(P, y, ln, env, sk);
       else ecs_exact<NT>(P, y, ln, env, sk);
     }
-    const uint32_t nd = pht_stream_pos(&ln.r);
+    /* draws: stream words; MHRS: + attempts (ln.neval, see mhrs_finish) */
+    const uint32_t nd = pht_stream_pos(&ln.r) + (METHOD == kMethodMHRS ? (uint32_t)ln.neval : 0u);
     if (DEBUG) {
       a.dbg_flags[i] = ln.flags;
       a.dbg_ndraw[i] = nd;
@@ -227,7 +424,7 @@ ecs_exact_kernel(SweepArgs a) {
   Lane ln;
 #ifdef PHT_STAMPS
   ln.st_last = __builtin_amdgcn_s_memtime();
-  for (int q = 0; q < 8; q++) ln.st_acc[q] = 0ull;
+  for (int q = 0; q < 15; q++) ln.st_acc[q] = 0ull;
   ln.st_rounds = 0ull;
 #endif
   EcsLane<NT> st;
@@ -337,18 +534,23 @@ ecs_exact_kernel(SweepArgs a) {
     if (need) pend = !ecs_jump_start(P, ln, env, sk, st, &pd);
 #else
     topup(need || pend);
+    PHT_STAMP(ln, 12);
     ecs_round(P, ln, env, sk, st, need, pend, pd, lam);
 #endif
   }
+#ifdef PHT_STAMPS
+  /* diagnostic builds: the extra words carry [rounds, 15 stamp slots] */
+  (void)c_obs; (void)c_neval; (void)c_flag; (void)c_nd; (void)c_jump;
+  if ((threadIdx.x & 63) == 0) {
+    lds_add(&xc[0], ln.st_rounds);
+    for (int q = 0; q < 15; q++) lds_add(&xc[1 + q], ln.st_acc[q]);
+  }
+#else
   lds_add(&xc[0], (unsigned long long)c_obs);
   lds_add(&xc[1], (unsigned long long)c_neval);
   lds_add(&xc[2], (unsigned long long)c_flag);
   lds_add(&xc[3], (unsigned long long)c_nd);
   lds_add(&xc[4], (unsigned long long)c_jump);
-#ifdef PHT_STAMPS
-  if ((threadIdx.x & 63) == 0)
-    for (int q = 0; q < 8; q++) lds_add(&xc[8 + q], ln.st_acc[q]);
-  if ((threadIdx.x & 63) == 0) lds_add(&xc[6], ln.st_rounds);
 #endif
   __syncthreads();
   unsigned long long *g = a.stats;
@@ -558,6 +760,40 @@ static hipError_t launch_ecs_group(const SweepArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
+/* the MHRS attempt search: round 0, rounds 1-5 (compaction after the
+ * multi-wavefront rounds); queue counts stay on the device (no host sync) */
+template <int NT>
+static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
+    cus = prop.multiProcessorCount;
+  }
+  if (a.mbest == nullptr || a.mq0 == nullptr || a.mq1 == nullptr || a.mcnt == nullptr || a.begin != 0)
+    return hipErrorInvalidValue;
+  const int sm = make_layout(a.n).bytes();
+  const long tasks = a.count * (1 + a.mhit);
+  if (hipMemsetAsync(a.mcnt, 0, sizeof(unsigned) * kMhrsCounters, st) != hipSuccess) return hipErrorUnknown;
+  hipLaunchKernelGGL((mhrs_round0<NT>), dim3((unsigned)((tasks + kBlock - 1) / kBlock)), dim3(kBlock), sm, st, a);
+  const dim3 grid((unsigned)(cus * 4));
+  unsigned *c = a.mcnt;
+  constexpr MhrsRound R1 = kMhrsRounds[0], R2 = kMhrsRounds[1], R3 = kMhrsRounds[2], R4 = kMhrsRounds[3],
+                      R5 = kMhrsRounds[4];
+  hipLaunchKernelGGL((mhrs_round<NT, R1.W, R1.K>), grid, dim3(kBlock), sm, st, a, R1.A0, a.mq0, c + 0, a.mq1, c + 1);
+  hipLaunchKernelGGL((mhrs_round<NT, R2.W, R2.K>), grid, dim3(kBlock), sm, st, a, R2.A0, a.mq1, c + 1, a.mq0, c + 2);
+  hipLaunchKernelGGL((mhrs_round<NT, R3.W, R3.K>), grid, dim3(kBlock), sm, st, a, R3.A0, a.mq0, c + 2, nullptr,
+                     nullptr);
+  hipLaunchKernelGGL(mhrs_compact, dim3(64), dim3(kBlock), 0, st, a, a.mq0, c + 2, a.mq1, c + 3);
+  hipLaunchKernelGGL((mhrs_round<NT, R4.W, R4.K>), grid, dim3(kBlock), sm, st, a, R4.A0, a.mq1, c + 3, nullptr,
+                     nullptr);
+  hipLaunchKernelGGL(mhrs_compact, dim3(64), dim3(kBlock), 0, st, a, a.mq1, c + 3, a.mq0, c + 4);
+  hipLaunchKernelGGL((mhrs_round<NT, R5.W, R5.K>), grid, dim3(kBlock), sm, st, a, R5.A0, a.mq0, c + 4, nullptr,
+                     nullptr);
+  return hipGetLastError();
+}
+
 template <int NT>
 static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStream_t st) {
   if (method == kMethodECS && a.cens == nullptr) { /* exact-only range */
@@ -571,6 +807,7 @@ static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStrea
   const int sm = smem_bytes(a.n);
 #define PHT_LAUNCH(M, D) hipLaunchKernelGGL((sweep_kernel<NT, M, D>), dim3(blocks), dim3(kBlock), sm, st, a)
   if (method == kMethodMHRS) {
+    if (hipError_t e = launch_mhrs_search<NT>(a, st); e != hipSuccess) return e;
     if (debug) PHT_LAUNCH(kMethodMHRS, true); else PHT_LAUNCH(kMethodMHRS, false);
   } else if (method == kMethodDCS) {
     if (debug) PHT_LAUNCH(kMethodDCS, true); else PHT_LAUNCH(kMethodDCS, false);

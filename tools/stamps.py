@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-phase cycle breakdown of the ECS exact kernel from a PHT_STAMPS build
+"""Per-phase cycle breakdown (wave-level s_memtime stamps; the stats block's
+extra words carry [rounds, 15 stamp slots] in PHT_STAMPS builds) of the ECS exact kernel from a PHT_STAMPS build
 (diagnostic only: stamps perturb the schedule; read shares, not totals).
 usage: PHT_LIB=/path/variant.so python3 tools/stamps.py [--N 1000000]"""
 import argparse
@@ -30,12 +31,12 @@ zexp = P.zexp_for(y)
 sw.sweep(S, s, zexp=zexp)
 st = sw.sweep(S, s, key=(3, 4), zexp=zexp)
 ex = st[2 * a.n + a.n * a.n:]
-names = ["phaseA_absorb_newobs", "start_evals_insert", "test_metropolis", "movemass_finish", "meets_cumulate",
-         "f0_cap", "invert", "proposal_eval"]
-tot = float(sum(ex[8:16]))
-rounds = float(ex[6])
-print(json.dumps({"kernel_ms": sw.last_kernel_ms(), "counters": ex[:8].tolist(),
-                  "wave_rounds": rounds,
-                  "cycles_per_round": {k: float(v) / max(rounds, 1) for k, v in zip(names, ex[8:16])},
-                  "shares": {k: float(v) / tot for k, v in zip(names, ex[8:16])},
-                  "evals_per_jump": float(ex[1]) / max(1, ex[4]), "jumps_per_obs": float(ex[4]) / a.N}, indent=1))
+names = ["phaseA_absorb_newobs", "dens_load_E0", "start_init4", "pend_insert", "meets", "cumulate", "f0_cap",
+         "invert_u", "proposal_eval", "test_metropolis", "big_general", "finish_movemass", "topup"]
+rounds = float(ex[0])
+cyc = [float(v) for v in ex[1:1 + len(names)]]
+tot = sum(cyc)
+print(json.dumps({"kernel_ms": sw.last_kernel_ms(), "N": a.N, "wave_rounds": rounds,
+                  "cycles_per_wave_round": round(tot / max(rounds, 1), 1),
+                  "cycles_per_round": {k: round(v / max(rounds, 1), 1) for k, v in zip(names, cyc)},
+                  "shares": {k: round(v / tot, 4) for k, v in zip(names, cyc)}}, indent=1))
