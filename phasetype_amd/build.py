@@ -1,7 +1,8 @@
 """Build the native library in-tree: phasetype_amd/_lib/libPhaseType.so.
 
-One hipcc invocation for gfx950: HIP kernels (pht_kernels.hip), the host
-runtime / C ABI (gibbs_host.cpp) and the R-compatible stream (rstream.c).
+hipcc for gfx950: the HIP kernels (pht_kernels_nt.hip once per compile-time
+n, in parallel, + the pht_dispatch.hip launcher), the host runtime / C ABI
+(gibbs_host.cpp) and the R-compatible stream (rstream.c), then one link.
 ``-ffp-contract=off`` is required: the device path must reproduce the
 oracle's arithmetic bit for bit (no implicit FMA contraction anywhere).
 """
@@ -11,14 +12,20 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(OUT_DIR, "libPhaseType.so")
-SOURCES = ["pht_kernels.hip", "gibbs_host.cpp", "rstream.c"]
-HEADERS = ["pht_device.h", "pht_env.h", "pht_kernels.h", "pht_layout.h", "rstream.h", "pht_ecs_round.h", "pht_ecs_group.h"]
+KERNEL_NTS = (10, 3, 5, 15, 20, 0)  # compile-time n of the kernels (0 = runtime n)
+# (source, extra defines) per object
+UNITS = [("pht_kernels_nt.hip", (f"PHT_NT={k}",)) for k in KERNEL_NTS] + [
+    ("pht_dispatch.hip", ()), ("gibbs_host.cpp", ()), ("rstream.c", ())]
+SOURCES = sorted({u[0] for u in UNITS})
+HEADERS = ["pht_device.h", "pht_env.h", "pht_kernels.h", "pht_kernels_impl.h", "pht_layout.h", "rstream.h",
+           "pht_ecs_round.h", "pht_ecs_group.h"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 DEFAULT_DEFINES: tuple = ("PHT_DETMATH_LDS", "PHT_ENV_K=9")
 
@@ -53,12 +60,13 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
     if not force and not defines and out is None and not needs_build():
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
-    objs = []
-    for src in SOURCES:
+
+    def compile_unit(idx_unit):
+        idx, (src, extra) = idx_unit
         path = os.path.join(CSRC, src)
-        obj = os.path.join(OUT_DIR, os.path.basename(target) + "." + src + ".o")
+        obj = os.path.join(OUT_DIR, f"{os.path.basename(target)}.{idx}.{src}.o")
         cmd = [_hipcc(), "-O3", "-fPIC", "-ffp-contract=off", f"-I{os.path.join(REPO, 'include')}", f"-I{CSRC}",
-               "-Wno-pass-failed"] + [f"-D{d}" for d in _merge_defines(defines)]
+               "-Wno-pass-failed"] + [f"-D{d}" for d in _merge_defines(tuple(defines) + tuple(extra))]
         if src.endswith(".hip"):
             cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-std=c++17"]
         elif src.endswith(".cpp"):
@@ -69,7 +77,11 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-        objs.append(obj)
+        return obj
+
+    workers = max(1, min(len(UNITS), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 8))
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        objs = list(ex.map(compile_unit, enumerate(UNITS)))
     tmp = target + ".tmp"
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + ["-ldl"]
     subprocess.run(cmd, check=True)

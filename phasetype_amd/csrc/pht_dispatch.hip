@@ -1,0 +1,33 @@
+/*
+ * pht_dispatch.hip — pht_launch_sweep: validates the launch and picks the
+ * kernels compiled for this n (pht_kernels_nt.hip; fully unrolled spectral
+ * sums for n in {3, 5, 10, 15, 20}, runtime-n loops otherwise).
+ */
+#include <hip/hip_runtime.h>
+
+#include "pht_kernels.h"
+#include "pht_layout.h"
+
+#define PHT_DECL(K) \
+  extern "C" hipError_t pht_launch_nt_##K(const pht::SweepArgs *a, int method, int debug, hipStream_t st);
+PHT_DECL(0)
+PHT_DECL(3)
+PHT_DECL(5)
+PHT_DECL(10)
+PHT_DECL(15)
+PHT_DECL(20)
+#undef PHT_DECL
+
+extern "C" hipError_t pht_launch_sweep(const pht::SweepArgs *a, int method, int debug, hipStream_t st) {
+  using namespace pht;
+  if (a->n < 1 || a->n > kMaxN) return hipErrorInvalidValue;
+  if ((make_layout(a->n).bytes() & 15) != 0) return hipErrorInvalidValue;
+  switch (a->n) {
+    case 3: return pht_launch_nt_3(a, method, debug, st);
+    case 5: return pht_launch_nt_5(a, method, debug, st);
+    case 10: return pht_launch_nt_10(a, method, debug, st);
+    case 15: return pht_launch_nt_15(a, method, debug, st);
+    case 20: return pht_launch_nt_20(a, method, debug, st);
+    default: return pht_launch_nt_0(a, method, debug, st);
+  }
+}

@@ -1,5 +1,7 @@
 /*
- * pht_kernels.hip — the Gibbs "step 1" sweep kernels for gfx950.
+ * pht_kernels_impl.h — the Gibbs "step 1" sweep kernels for gfx950
+ * (templates; instantiated per compile-time n by pht_kernels_nt.hip, one
+ * translation unit per n so that they compile in parallel).
  *
  * One lane = one observation (SURVEY.md §8e sharding).  A workgroup stages
  * the packed per-sweep parameter block (pht_layout.h) into LDS once, each
@@ -13,6 +15,8 @@
  * Replaces, per sweep: LJMA_MHsample_Bladt / LJMA_MHsample_Aslett2 /
  * LJMA_MHsample_Hobolth2 (src/PHT_MCMC_Aslett.c:325-333).
  */
+#ifndef PHT_KERNELS_IMPL_H
+#define PHT_KERNELS_IMPL_H
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -213,7 +217,9 @@ __global__ void __launch_bounds__(kBlock) mhrs_round(SweepArgs a, uint32_t A0, c
   }
 }
 
-/* tasks of qin still unresolved -> qout */
+/* tasks of qin still unresolved -> qout (templated only to keep one copy
+ * per pht_kernels_nt.hip unit) */
+template <int NT>
 __global__ void __launch_bounds__(kBlock) mhrs_compact(SweepArgs a, const uint32_t *qin, const unsigned *cin,
                                                        uint32_t *qout, unsigned *cout) {
   const long cnt = *cin;
@@ -785,10 +791,10 @@ static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
   hipLaunchKernelGGL((mhrs_round<NT, R2.W, R2.K>), grid, dim3(kBlock), sm, st, a, R2.A0, a.mq1, c + 1, a.mq0, c + 2);
   hipLaunchKernelGGL((mhrs_round<NT, R3.W, R3.K>), grid, dim3(kBlock), sm, st, a, R3.A0, a.mq0, c + 2, nullptr,
                      nullptr);
-  hipLaunchKernelGGL(mhrs_compact, dim3(64), dim3(kBlock), 0, st, a, a.mq0, c + 2, a.mq1, c + 3);
+  hipLaunchKernelGGL((mhrs_compact<NT>), dim3(64), dim3(kBlock), 0, st, a, a.mq0, c + 2, a.mq1, c + 3);
   hipLaunchKernelGGL((mhrs_round<NT, R4.W, R4.K>), grid, dim3(kBlock), sm, st, a, R4.A0, a.mq1, c + 3, nullptr,
                      nullptr);
-  hipLaunchKernelGGL(mhrs_compact, dim3(64), dim3(kBlock), 0, st, a, a.mq1, c + 3, a.mq0, c + 4);
+  hipLaunchKernelGGL((mhrs_compact<NT>), dim3(64), dim3(kBlock), 0, st, a, a.mq1, c + 3, a.mq0, c + 4);
   hipLaunchKernelGGL((mhrs_round<NT, R5.W, R5.K>), grid, dim3(kBlock), sm, st, a, R5.A0, a.mq0, c + 4, nullptr,
                      nullptr);
   return hipGetLastError();
@@ -797,9 +803,11 @@ static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
 template <int NT>
 static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStream_t st) {
   if (method == kMethodECS && a.cens == nullptr) { /* exact-only range */
-    if (a.group == 4) return debug ? launch_ecs_group<NT, 4, true>(a, st) : launch_ecs_group<NT, 4, false>(a, st);
-    if (a.group == 2) return debug ? launch_ecs_group<NT, 2, true>(a, st) : launch_ecs_group<NT, 2, false>(a, st);
-    if (a.group == 8) return debug ? launch_ecs_group<NT, 8, true>(a, st) : launch_ecs_group<NT, 8, false>(a, st);
+    /* lane groups (opt-in, PHT_GROUP): compiled for n = 10 and runtime n */
+    constexpr int GT = (NT == 10) ? 10 : 0;
+    if (a.group == 4) return debug ? launch_ecs_group<GT, 4, true>(a, st) : launch_ecs_group<GT, 4, false>(a, st);
+    if (a.group == 2) return debug ? launch_ecs_group<GT, 2, true>(a, st) : launch_ecs_group<GT, 2, false>(a, st);
+    if (a.group == 8) return debug ? launch_ecs_group<GT, 8, true>(a, st) : launch_ecs_group<GT, 8, false>(a, st);
     return debug ? launch_ecs_exact<NT, true>(a, st) : launch_ecs_exact<NT, false>(a, st);
   }
   const int blocks = (int)((a.count + kBlock - 1) / kBlock);
@@ -819,14 +827,4 @@ static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStrea
 }
 
 }  // namespace pht
-
-extern "C" hipError_t pht_launch_sweep(const pht::SweepArgs *a, int method, int debug, hipStream_t st) {
-  using namespace pht;
-  if (a->n < 1 || a->n > kMaxN) return hipErrorInvalidValue;
-  if ((make_layout(a->n).bytes() & 15) != 0) return hipErrorInvalidValue;
-  switch (a->n) {
-    case 3: return launch_nt<3>(*a, method, debug != 0, st);
-    case 10: return launch_nt<10>(*a, method, debug != 0, st);
-    default: return launch_nt<0>(*a, method, debug != 0, st);
-  }
-}
+#endif
