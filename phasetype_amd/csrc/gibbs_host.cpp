@@ -503,6 +503,9 @@ static int exact_group(const pht_ctx *c) {
   return 0;
 }
 
+/* lanes of the persistent ECS grid on an MI355X (256 CUs x 2 blocks x 256) */
+constexpr long kSpreadLanes = 256L * 2 * 256;
+
 /* blocks per CU for the persistent ECS kernel (PHT_ECS_OCC forces it) */
 static int exact_occ(const pht_ctx *c) {
   if (const char *e = getenv("PHT_ECS_OCC")) return atoi(e);
@@ -565,6 +568,10 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     ae.cens = nullptr;
     ae.group = exact_group(c);
     ae.occ = exact_occ(c);
+    /* lane-major first claims when the shard is within ~2 observations per
+     * lane (the longest paths, one per wavefront; tools/latency.py:
+     * -10 % at 31k-125k per GPU); PHT_SPREAD=0|1 forces it */
+    ae.spread = getenv("PHT_SPREAD") ? atoi(getenv("PHT_SPREAD")) : (c->n_exact <= 2 * kSpreadLanes);
     if (ae.count > 0) HIPCHK(pht_launch_sweep(&ae, c->method, debug ? 1 : 0, c->stream));
     SweepArgs ac = a;
     ac.begin = c->n_exact;

@@ -30,6 +30,7 @@ struct SweepArgs {
   unsigned long long *stats;   /* [stats_len(n)] int64, accumulated */
   int group;                   /* ECS exact: lanes per observation (0/1 = one lane; 2, 4, 8) */
   int occ;                     /* ECS exact: blocks per CU of the persistent grid (0 = occupancy limit) */
+  int spread;                  /* ECS exact: first claims lane-major (the longest paths one per wavefront) */
   /* MHRS attempt search (pht_kernels.hip, MHRS section): per chain task
    * (position * (1 + mhit) + c) its first success (attempt << 8 | pre), two
    * task queues and the queue counters; allocated by the host for MHRS */

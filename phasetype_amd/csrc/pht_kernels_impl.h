@@ -440,6 +440,11 @@ ecs_exact_kernel(SweepArgs a) {
    * observation ahead, so a refill never waits on global memory */
   auto claim = [&]() -> long {
     const long t = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    /* spread: a lane's first claim is lane-major over the grid's
+     * wavefronts, so the longest paths (the first positions) go one per
+     * wavefront instead of 64 to wavefront 0 */
+    if (a.spread && t < kBlock)
+      return (long)(t & 63) * ((long)gridDim.x * (kBlock / 64)) + (long)(t >> 6) * gridDim.x + blockIdx.x;
     return claim_pos(t);
   };
   long nextp = claim();

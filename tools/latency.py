@@ -26,8 +26,8 @@ from phasetype_amd.synth import DATA_KEY, bd_exit, bd_exit_structure, simulate_p
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=10)
-    ap.add_argument("--Ns", nargs="+", default=["top64", "top4096", "31250", "62500", "125000", "250000"])
-    ap.add_argument("--variants", nargs="+", default=["g1o2", "g1o1", "g2", "g4", "g8"])
+    ap.add_argument("--Ns", nargs="+", default=["top4096", "31250", "62500", "125000", "250000", "500000", "1000000"])
+    ap.add_argument("--variants", nargs="+", default=["g1o2", "sp", "g4"])
     ap.add_argument("--sweeps", type=int, default=8)
     a = ap.parse_args()
     n = a.n
@@ -51,7 +51,11 @@ def main():
         for v in a.variants:
             os.environ.pop("PHT_GROUP", None)
             os.environ.pop("PHT_ECS_OCC", None)
-            if v.startswith("g1o"):
+            os.environ.pop("PHT_SPREAD", None)
+            if v == "sp":
+                os.environ["PHT_GROUP"] = "1"
+                os.environ["PHT_SPREAD"] = "1"
+            elif v.startswith("g1o"):
                 os.environ["PHT_GROUP"] = "1"
                 os.environ["PHT_ECS_OCC"] = v[3:]
             else:
