@@ -571,6 +571,9 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     /* lane-major first claims when the shard is within ~2 observations per
      * lane (the longest paths, one per wavefront; tools/latency.py:
      * -10 % at 31k-125k per GPU); PHT_SPREAD=0|1 forces it */
+    /* one new observation per lane per round (PHT_NEWCAP=0: no limit;
+     * tools/latency.py: -2 % kernel time at 1e6) */
+    ae.newcap = getenv("PHT_NEWCAP") ? atoi(getenv("PHT_NEWCAP")) : 1;
     ae.spread = getenv("PHT_SPREAD") ? atoi(getenv("PHT_SPREAD")) : (c->n_exact <= 2 * kSpreadLanes);
     if (ae.count > 0) HIPCHK(pht_launch_sweep(&ae, c->method, debug ? 1 : 0, c->stream));
     SweepArgs ac = a;

@@ -31,6 +31,7 @@ struct SweepArgs {
   int group;                   /* ECS exact: lanes per observation (0/1 = one lane; 2, 4, 8) */
   int occ;                     /* ECS exact: blocks per CU of the persistent grid (0 = occupancy limit) */
   int spread;                  /* ECS exact: first claims lane-major (the longest paths one per wavefront) */
+  int newcap;                  /* ECS exact: observations a lane may start per round (0 = no limit) */
   /* MHRS attempt search (pht_kernels.hip, MHRS section): per chain task
    * (position * (1 + mhit) + c) its first success (attempt << 8 | pre), two
    * task queues and the queue counters; allocated by the host for MHRS */

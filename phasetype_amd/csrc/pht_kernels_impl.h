@@ -489,12 +489,18 @@ ecs_exact_kernel(SweepArgs a) {
   for (;;) {
     bool need = false;
     topup(!pend);
+    int nnew = 0; /* observations started by this lane in this round */
     while (!done && !pend) {
       if (!have) {
         if (nextp >= a.count) {
           done = true;
           break;
         }
+        /* newcap: a lane starts at most that many observations per round
+         * (a path that ends at its first absorb test leaves the lane idle
+         * until the next round instead of running phase A again) */
+        if (a.newcap > 0 && nnew >= a.newcap) break;
+        nnew++;
         pos = a.begin + nextp;
         const double yobs = ny;
         const uint32_t gobs = ngid;

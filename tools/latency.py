@@ -52,7 +52,11 @@ def main():
             os.environ.pop("PHT_GROUP", None)
             os.environ.pop("PHT_ECS_OCC", None)
             os.environ.pop("PHT_SPREAD", None)
-            if v == "sp":
+            os.environ.pop("PHT_NEWCAP", None)
+            if v.startswith("nc"):
+                os.environ["PHT_GROUP"] = "1"
+                os.environ["PHT_NEWCAP"] = v[2:]
+            elif v == "sp":
                 os.environ["PHT_GROUP"] = "1"
                 os.environ["PHT_SPREAD"] = "1"
             elif v.startswith("g1o"):
