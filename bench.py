@@ -32,7 +32,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 import phasetype_amd as P  # noqa: E402
-from phasetype_amd.dist import make_stats_allreduce, max_over_ranks, shard_range  # noqa: E402
+from phasetype_amd.dist import make_stats_allreduce, max_over_ranks, shard_range, sum_over_ranks  # noqa: E402
 from phasetype_amd.synth import DATA_KEY, bd_exit, bd_exit_structure, simulate_ph  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--method", default="ECS", choices=["ECS", "MHRS", "DCS"])
     ap.add_argument("--censor", type=float, default=0.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling side measurement (N > 1)")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_latest.json"))
     args = ap.parse_args()
 
@@ -153,6 +154,30 @@ def main():
         dt, kernel_ms = max_over_ranks(dist, [dt, kernel_ms], device=coll_dev)
     if not np.all(np.isfinite(res)):
         raise SystemExit("non-finite Gibbs draws")
+    sw.close()
+
+    weak = None
+    if dist is not None and not args.no_weak:
+        # Side measurement (not `value`): weak scaling, every rank holding N
+        # observations of its own (one chain over world x N observations).
+        yw, cw = simulate_ph(S, s, N, seed=DATA_KEY + 1 + rank, censor_frac=args.censor)
+        tot = sum_over_ranks(dist, [float(np.sum(yw))], device=coll_dev)[0]
+        zexp_w = P.zexp_for(np.array([tot]))
+        sw2 = P.Sweeper(n, method, 1, device=local)
+        sw2.set_obs(yw, cw, obs0=rank * N)
+        P.set_seed(20241009)
+        warm = sw2.gibbs(args.warmup + 1, method, nu, zeta, T, Cm, zexp_w, reduce=reduce)
+        sync()
+        t1 = time.perf_counter()
+        sw2.gibbs(args.steps + 1, method, nu, zeta, T, Cm, zexp_w, start=warm[-1], reduce=reduce)
+        sync()
+        dtw = max_over_ranks(dist, [time.perf_counter() - t1], device=coll_dev)[0]
+        sw2.close()
+        weak = {"N_per_gpu": N, "N_total": N * world, "chain_sweeps_per_s": args.steps / dtw,
+                "value": world * args.steps / dtw, "unit": f"{N:.0e}-observation sweeps/s (node)",
+                "ms_per_step": dtw / args.steps * 1e3,
+                "note": "side measurement: one chain over world x N observations (each rank N of its own); "
+                        "value = world x chain sweeps/s; `value` above is the BASELINE metric (strong, N fixed)"}
 
     if rank == 0:
         sweeps_per_s = args.steps / dt
@@ -196,6 +221,8 @@ def main():
                                      "unit": "TFLOP/s", "frac": tfs / FP64_VALU_PEAK_TF,
                                      "note": "FP64 lane-flops per launch from PMC (SQ_INSTS_VALU_FLOPS_FP64 x 64 x "
                                              "VALU lane utilisation, profiles/traffic_latest.json) / kernel time"}
+        if weak is not None:
+            line["weak_scaling"] = weak
         if world == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(n, y, cen, T, nu, zeta)

@@ -48,3 +48,12 @@ def max_over_ranks(dist, values, device: str = "cpu"):
     t = torch.tensor(list(values), dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(v) for v in t.cpu()]
+
+
+def sum_over_ranks(dist, values, device: str = "cpu"):
+    """Element-wise sum of a few floats over ranks."""
+    import torch
+
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    return [float(v) for v in t.cpu()]

@@ -43,7 +43,7 @@ def _worker(rank, world, port, cases):
     import torch.distributed as dist
 
     from oracle.oracle import OracleLib
-    from phasetype_amd.dist import make_stats_allreduce, max_over_ranks
+    from phasetype_amd.dist import make_stats_allreduce, max_over_ranks, sum_over_ranks
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
@@ -64,6 +64,8 @@ def _worker(rank, world, port, cases):
                 assert np.array_equal(st, want), (rank, n, method, sweep)
         mx = max_over_ranks(dist, [float(rank), -float(rank)])
         assert mx == [float(world - 1), 0.0]
+        sm = sum_over_ranks(dist, [float(rank + 1)])
+        assert sm == [world * (world + 1) / 2.0]
         dist.barrier()
     finally:
         dist.destroy_process_group()

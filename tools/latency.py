@@ -38,7 +38,10 @@ def main():
     zexp = P.zexp_for(y)
     Cm = np.ones(T.shape)
     for spec in a.Ns:
-        if spec.startswith("top"):
+        if spec.startswith("rand"):
+            k = int(spec[4:])
+            idx = np.sort(np.random.default_rng(11).choice(len(y), k, replace=False))
+        elif spec.startswith("top"):
             k = int(spec[3:])
             idx = np.sort(np.argsort(-y)[:k])
         else:
