@@ -452,15 +452,15 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
   if (count == 0) return 0;
   std::vector<long> ord(count);
   std::iota(ord.begin(), ord.end(), 0L);
-  /* exact observations by decreasing y: the persistent kernel hands out
-   * long paths first and ends on short ones (a short tail); censored ones
-   * (one lane per observation) by increasing y.  PHT_ORDER=asc|none: A/B. */
+  /* exact observations, then censored ones, each by decreasing y: the
+   * persistent kernels hand out long paths first and end on short ones (a
+   * short tail).  PHT_ORDER=asc|none: A/B of the exact range. */
   const char *oe = getenv("PHT_ORDER");
   const int omode = !oe ? 0 : (!strcmp(oe, "asc") ? 1 : (!strcmp(oe, "none") ? 2 : 0));
   std::stable_sort(ord.begin(), ord.end(), [&](long a, long b) {
     const int ca = cens[a] != 0, cb = cens[b] != 0;
     if (ca != cb) return ca < cb;
-    if (ca) return y[a] < y[b];
+    if (ca) return y[a] > y[b];
     if (omode == 2) return false;
     return omode == 1 ? (y[a] < y[b]) : (y[a] > y[b]);
   });

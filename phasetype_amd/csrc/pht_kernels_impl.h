@@ -273,7 +273,11 @@ __device__ __forceinline__ void mhrs_finish(const Par<NT> &P, const SweepArgs &a
   ln.neval = (int)natt;
 }
 
-template <int NT, int METHOD, bool DEBUG, class Env>
+/* One lane per observation (PERSIST false: lane = launch position), or
+ * persistent lanes (PERSIST true: a lane claims the next 64-position chunk
+ * slot through an LDS cursor as soon as its observation is done, so a
+ * wavefront never waits on its longest path; DCS and the censored range). */
+template <int NT, int METHOD, bool DEBUG, class Env, bool PERSIST = false>
 __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
@@ -290,9 +294,11 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
   PHT_LDS unsigned long long *xc = zq + n; /* kStatExtra counters */
   PHT_LDS unsigned *Bc = (PHT_LDS unsigned *)(xc + kStatExtra);
   PHT_LDS unsigned *Nc = Bc + n;
+  PHT_LDS int *cursor = (PHT_LDS int *)(Nc + n * n);
   pht_stage_math_tables();
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
+  if (PERSIST && threadIdx.x == 0) *cursor = 0;
   __syncthreads();
 
   Par<NT> P;
@@ -300,8 +306,16 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
   P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
   P.Lr = L;
 
-  const long i = a.begin + (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < a.begin + a.count) {
+  long i = a.begin + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (;;) {
+    if (PERSIST) {
+      const long t = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const long p = claim_pos(t);
+      if (p >= a.count) break;
+      i = a.begin + p;
+    } else if (i >= a.begin + a.count) {
+      break;
+    }
     Lane ln;
     pht_stream_init(&ln.r, a.k0, a.k1, a.gid[i], 0u, a.sweep);
     ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
@@ -334,6 +348,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
     lds_add(&xc[3], (unsigned long long)nd);
     lds_add(&xc[4], (unsigned long long)ln.njump);
     lds_add(&xc[5], (unsigned long long)ln.nbrent);
+    if (!PERSIST) break;
   }
   __syncthreads();
   /* flush: [zq n][B n][N n*n][extra] */
@@ -353,10 +368,39 @@ __global__ void __launch_bounds__(kBlock) sweep_kernel(SweepArgs a) {
   sweep_body<NT, METHOD, DEBUG, EnvPrivate>(a);
 }
 
-/* LDS bytes a workgroup needs: parameter block + accumulators */
+template <int NT, int METHOD, bool DEBUG>
+__global__ void __launch_bounds__(kBlock) persist_kernel(SweepArgs a) {
+  sweep_body<NT, METHOD, DEBUG, EnvPrivate, true>(a);
+}
+
+/* LDS bytes a workgroup needs: parameter block + accumulators (+ cursor) */
 static int smem_bytes(int n) {
   const Layout L = make_layout(n);
-  return L.bytes() + (n + kStatExtra) * 8 + (n + n * n) * 4;
+  return L.bytes() + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4;
+}
+
+/* persistent one-lane kernels: grid = CUs x occupancy, capped by the work */
+template <int NT, int METHOD, bool DEBUG>
+static hipError_t launch_persist(const SweepArgs &a, hipStream_t st) {
+  static int occ = -1, cus = 0;
+  const int sm = smem_bytes(a.n);
+  if (occ < 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
+    cus = prop.multiProcessorCount;
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, persist_kernel<NT, METHOD, DEBUG>, kBlock, sm) != hipSuccess ||
+        b < 1)
+      b = 1;
+    occ = b;
+  }
+  long grid = (long)cus * occ;
+  const long want = (a.count + kBlock - 1) / kBlock;
+  if (grid > want) grid = want;
+  if (grid < 1) return hipSuccess;
+  hipLaunchKernelGGL((persist_kernel<NT, METHOD, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
+  return hipGetLastError();
 }
 
 /*
@@ -829,9 +873,9 @@ static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStrea
     if (hipError_t e = launch_mhrs_search<NT>(a, st); e != hipSuccess) return e;
     if (debug) PHT_LAUNCH(kMethodMHRS, true); else PHT_LAUNCH(kMethodMHRS, false);
   } else if (method == kMethodDCS) {
-    if (debug) PHT_LAUNCH(kMethodDCS, true); else PHT_LAUNCH(kMethodDCS, false);
+    return debug ? launch_persist<NT, kMethodDCS, true>(a, st) : launch_persist<NT, kMethodDCS, false>(a, st);
   } else {
-    if (debug) PHT_LAUNCH(kMethodECS, true); else PHT_LAUNCH(kMethodECS, false);
+    return debug ? launch_persist<NT, kMethodECS, true>(a, st) : launch_persist<NT, kMethodECS, false>(a, st);
   }
 #undef PHT_LAUNCH
   return hipGetLastError();
