@@ -85,11 +85,11 @@ __device__ __forceinline__ long claim_pos(long t) {
  * probability is p needs ~1/p attempts and p is ~uniform over the data
  * (a few tasks per sweep need ~1e5-1e6 attempts, the reference's whole
  * run time; one lane per observation would serialise them):
- *   round 0  one lane per task, attempts [0, 16)             (mhrs_round0)
- *   round r  W lanes per unresolved task, 16-32 steps of W attempts
- *            (W = 8, 64: one wavefront segment per task, ballot per step;
- *             W = 1024, 16384, 131072: atomicMin on the task's record, early
- *             exit once it is below the lane's next attempt)
+ *   round 0  one lane per task, attempts [0, 16)
+ *   round r  W = 8, 64, 1024, 16384, 131072 lanes per unresolved task,
+ *            K = 16 (32) attempts each: attempt A0 + l + W k for lane l
+ * (mhrs_search: jump-converged, the tasks' records lowered by atomicMin;
+ * mhrs_compact collects the unresolved tasks between rounds).
  * Attempt streams are per (task, attempt), so the first success does not
  * depend on which lane tried what.  mhrs_finish then makes the MH decisions
  * (tag-0 stream) and replays the accepted attempt for the statistics.
@@ -116,103 +116,130 @@ __device__ __forceinline__ Par<NT> stage_params(const SweepArgs &a, PHT_LDS unsi
   return P;
 }
 
-/* round 0: one lane per task; unresolved tasks -> mq0 (count mcnt[0]) */
-template <int NT>
-__global__ void __launch_bounds__(kBlock) mhrs_round0(SweepArgs a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const Par<NT> P = stage_params<NT>(a, (PHT_LDS unsigned char *)smem);
-  pht_stage_math_tables();
-  __syncthreads();
-  const int T1 = 1 + a.mhit;
-  const long task = (long)blockIdx.x * kBlock + threadIdx.x;
-  if (task >= a.count * T1) return;
-  const long pos = task / T1;
-  const int c = (int)(task % T1);
-  const int cens = a.cens[pos];
-  if (c > 0 && cens) { /* censored observations have no proposals */
-    a.mbest[task] = 0u;
-    return;
-  }
-  const double y = a.y[pos];
-  const uint32_t gid = a.gid[pos];
-  for (uint32_t att = 0; att < (uint32_t)kMhrsK0; att++) {
-    int pre = 0;
-    if (mhrs_try<NT>(P, y, cens, a.k0, a.k1, gid, a.sweep, c, att, pre)) {
-      a.mbest[task] = mhrs_pack(att, pre);
-      return;
-    }
-  }
-  a.mbest[task] = kMhrsUnresolved;
-  a.mq0[atomicAdd(&a.mcnt[0], 1u)] = (uint32_t)task;
-}
-
-/* round with W lanes per task over the tasks in qin[0 .. *cin); W <= 64:
- * unresolved tasks are appended to qout (count *cout) */
+/*
+ * Jump-converged search round: each lane works through items (task, l) of
+ * the round, i.e. attempts A0 + l + W k (k < K) of the task, one JUMP per
+ * loop iteration; a lane whose attempt ends starts its next attempt (or
+ * item) in the next iteration, so a wavefront never waits for its longest
+ * attempt.  A success lowers the task's record with atomicMin; a lane skips
+ * attempts above the record (it tries its own attempts in increasing order,
+ * so every attempt below the final record is tried: first success exact).
+ * qin == nullptr: all tasks (round 0; the censored observations' proposal
+ * tasks are marked resolved).  Unresolved tasks are collected afterwards by
+ * mhrs_compact.
+ */
 template <int NT, int W, int K>
-__global__ void __launch_bounds__(kBlock) mhrs_round(SweepArgs a, uint32_t A0, const uint32_t *qin,
-                                                     const unsigned *cin, uint32_t *qout, unsigned *cout) {
+__global__ void __launch_bounds__(kBlock) mhrs_search(SweepArgs a, uint32_t A0, const uint32_t *qin,
+                                                      const unsigned *cin) {
   extern __shared__ __align__(16) unsigned char smem[];
   const Par<NT> P = stage_params<NT>(a, (PHT_LDS unsigned char *)smem);
+  /* items are claimed one at a time through an LDS cursor (claim_pos: the
+   * block's 64-item chunks), so a lane whose item ends takes the next one
+   * and the wavefront stays full until the round's items run out */
+  PHT_LDS int *cursor = (PHT_LDS int *)((PHT_LDS unsigned char *)smem + make_layout(a.n).bytes());
+  if (threadIdx.x == 0) *cursor = 0;
   pht_stage_math_tables();
   __syncthreads();
+  const int n = P.n();
   const int T1 = 1 + a.mhit;
-  const long total = (long)(*cin) * W;
-  const int lane = threadIdx.x & 63;
-  const long gsize = (long)gridDim.x * kBlock;
-  /* wave-uniform loop: a wavefront holds 64 consecutive items (W | 64 keeps
-   * a task's lanes in one wavefront segment) */
-  for (long b = (long)blockIdx.x * kBlock + (threadIdx.x & ~63); b < total; b += gsize) {
-    const long item = b + lane;
-    const bool live = item < total;
-    uint32_t task = 0;
-    int c = 0, cens = 0, l = 0;
-    double y = 0.0;
-    uint32_t gid = 0;
-    if (live) {
-      task = qin[item / W];
-      l = (int)(item % W);
-      const long pos = task / T1;
-      c = (int)(task % T1);
-      y = a.y[pos];
-      cens = a.cens[pos];
-      gid = a.gid[pos];
-    }
-    bool act = live, found = false;
-    const int seg0 = (W >= 64) ? 0 : (lane & ~(W - 1));
-    for (int k = 0; k < K; k++) {
-      const uint32_t att = A0 + (uint32_t)l + (uint32_t)W * (uint32_t)k;
-      if (att >= (uint32_t)kMhrsMaxAtt) act = false;
-      if constexpr (W > 64) {
-        if (act) {
-          const uint32_t cur = __hip_atomic_load(&a.mbest[task], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((cur >> 8) < att) act = false;
+  const long total = (qin ? (long)(*cin) : a.count * T1) * W;
+  long item = 0;
+  /* item state */
+  bool have = false;
+  uint32_t task = 0, gid = 0;
+  int c = 0, cens = 0, l = 0, k = 0;
+  double y = 0.0;
+  /* attempt state */
+  bool inatt = false, fresh = false;
+  pht_stream r;
+  double t = 0.0;
+  int j = 0, lastj = 0, nj = 0;
+  uint32_t att = 0;
+  for (;;) {
+    while (!inatt) { /* next attempt of this item, or the next item */
+      if (!have) {
+        if (item >= total) break;
+        item = claim_pos(__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (item >= total) break;
+        const long q = item / W;
+        l = (int)(item % W);
+        task = qin ? qin[q] : (uint32_t)q;
+        const long pos = task / T1;
+        c = (int)(task % T1);
+        cens = a.cens[pos];
+        if (c > 0 && cens) { /* censored observations have no proposals */
+          if (l == 0) a.mbest[task] = 0u;
+          continue;
         }
-        if (!__any(act)) break;
+        y = a.y[pos];
+        gid = a.gid[pos];
+        k = 0;
+        have = true;
       }
-      int pre = 0;
-      const bool ok = act && mhrs_try<NT>(P, y, cens, a.k0, a.k1, gid, a.sweep, c, att, pre);
-      if constexpr (W <= 64) {
-        const unsigned long long m = __ballot(ok);
-        const unsigned long long segm = (W >= 64) ? ~0ull : (((1ull << W) - 1ull) << seg0);
-        const unsigned long long sm = m & segm;
-        const int first = sm ? (__ffsll((long long)sm) - 1) : lane;
-        const int fpre = __shfl(pre, first);
-        if (sm) {
-          if (live && lane == seg0 && !found)
-            a.mbest[task] = mhrs_pack(A0 + (uint32_t)(first - seg0) + (uint32_t)W * (uint32_t)k, fpre);
-          found = true;
-          act = false;
-        }
-        if (!__any(act)) break;
-      } else {
-        if (ok) {
-          atomicMin(&a.mbest[task], mhrs_pack(att, pre));
-          act = false;
+      if (k >= K) {
+        have = false;
+        continue;
+      }
+      att = A0 + (uint32_t)l + (uint32_t)W * (uint32_t)k;
+      k++;
+      if (att >= (uint32_t)kMhrsMaxAtt ||
+          (__hip_atomic_load(&a.mbest[task], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 8) < att) {
+        have = false;
+        continue;
+      }
+      /* the stream's blocks come from the converged top-up below */
+      pht_stream_init(&r, a.k0, a.k1, gid, mhrs_tag(c, att), a.sweep);
+      fresh = true;
+      inatt = true;
+    }
+    if (!__any(inatt)) break;
+    /* converged Philox: every lane with an attempt generates its next block
+     * here, once per iteration, instead of inside the draws (where only the
+     * lanes whose buffer ran dry would, one draw site at a time); a step
+     * uses at most 4 words (start draw + a jump's 3), and the buffer then
+     * holds >= 4 (same word sequence either way) */
+    if (inatt) pht_stream_topup(&r);
+    if (inatt && fresh) { /* start state of the attempt */
+      const double target = pht_next_u(&r);
+      double sofar = 0.0;
+      int B2 = 0;
+      while (sofar < target && B2 <= n) sofar += (B2 < n ? P.pi(B2) : 0.0), B2++;
+      j = lastj = B2 - 1;
+      t = 0.0;
+      nj = 0;
+      fresh = false;
+    }
+    if (inatt) {
+      /* one jump of mhrs_attempt (pht_device.h) */
+      if ((t < y && j < n) || (cens && j < n)) {
+        if (nj++ >= kMaxJumps) {
+          t = y;
+          j = n; /* ends the attempt; t >= y: accepted as in mhrs_attempt */
+        } else {
+          t = t + dev_rexp(r, 1.0 / -P.S(j, j));
+          const double target = pht_next_u(&r);
+          const int cnt = P.nsuccPf(j);
+          double sofar = 0.0;
+          int sel = n + 1;
+          for (int q = 0; q < cnt; q++) {
+            const int kk = P.succPf(j, q);
+            sofar += P.Pf(j, kk);
+            if (!(sofar < target)) {
+              sel = kk;
+              break;
+            }
+          }
+          j = sel;
+          if ((t < y && j < n) || (cens && j < n)) lastj = j;
         }
       }
-    }
-    if constexpr (W <= 64) {
-      if (live && lane == seg0 && !found) qout[atomicAdd(cout, 1u)] = task;
+      if (!((t < y && j < n) || (cens && j < n))) {
+        inatt = false;
+        if (!(t < y) && lastj < n && P.s(lastj) > 0.0) {
+          atomicMin(&a.mbest[task], mhrs_pack(att, lastj));
+          have = false; /* this lane's further attempts are larger */
+        }
+      }
     }
   }
 }
@@ -222,9 +249,9 @@ __global__ void __launch_bounds__(kBlock) mhrs_round(SweepArgs a, uint32_t A0, c
 template <int NT>
 __global__ void __launch_bounds__(kBlock) mhrs_compact(SweepArgs a, const uint32_t *qin, const unsigned *cin,
                                                        uint32_t *qout, unsigned *cout) {
-  const long cnt = *cin;
+  const long cnt = qin ? (long)(*cin) : a.count * (1 + a.mhit);
   for (long q = (long)blockIdx.x * kBlock + threadIdx.x; q < cnt; q += (long)gridDim.x * kBlock) {
-    const uint32_t task = qin[q];
+    const uint32_t task = qin ? qin[q] : (uint32_t)q;
     if (a.mbest[task] == kMhrsUnresolved) qout[atomicAdd(cout, 1u)] = task;
   }
 }
@@ -837,21 +864,35 @@ static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
   const int sm = make_layout(a.n).bytes();
   const long tasks = a.count * (1 + a.mhit);
   if (hipMemsetAsync(a.mcnt, 0, sizeof(unsigned) * kMhrsCounters, st) != hipSuccess) return hipErrorUnknown;
-  hipLaunchKernelGGL((mhrs_round0<NT>), dim3((unsigned)((tasks + kBlock - 1) / kBlock)), dim3(kBlock), sm, st, a);
-  const dim3 grid((unsigned)(cus * 4));
-  unsigned *c = a.mcnt;
-  constexpr MhrsRound R1 = kMhrsRounds[0], R2 = kMhrsRounds[1], R3 = kMhrsRounds[2], R4 = kMhrsRounds[3],
-                      R5 = kMhrsRounds[4];
-  hipLaunchKernelGGL((mhrs_round<NT, R1.W, R1.K>), grid, dim3(kBlock), sm, st, a, R1.A0, a.mq0, c + 0, a.mq1, c + 1);
-  hipLaunchKernelGGL((mhrs_round<NT, R2.W, R2.K>), grid, dim3(kBlock), sm, st, a, R2.A0, a.mq1, c + 1, a.mq0, c + 2);
-  hipLaunchKernelGGL((mhrs_round<NT, R3.W, R3.K>), grid, dim3(kBlock), sm, st, a, R3.A0, a.mq0, c + 2, nullptr,
-                     nullptr);
-  hipLaunchKernelGGL((mhrs_compact<NT>), dim3(64), dim3(kBlock), 0, st, a, a.mq0, c + 2, a.mq1, c + 3);
-  hipLaunchKernelGGL((mhrs_round<NT, R4.W, R4.K>), grid, dim3(kBlock), sm, st, a, R4.A0, a.mq1, c + 3, nullptr,
-                     nullptr);
-  hipLaunchKernelGGL((mhrs_compact<NT>), dim3(64), dim3(kBlock), 0, st, a, a.mq1, c + 3, a.mq0, c + 4);
-  hipLaunchKernelGGL((mhrs_round<NT, R5.W, R5.K>), grid, dim3(kBlock), sm, st, a, R5.A0, a.mq0, c + 4, nullptr,
-                     nullptr);
+  {
+    const int smc = sm + 16; /* + the claim cursor */
+    /* persistent grid: exactly the resident blocks (a block that started
+     * late would still own its share of the claim chunks) */
+    static int occc = -1;
+    if (occc < 0) {
+      int b = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, mhrs_search<NT, 1, kMhrsK0>, kBlock, smc) != hipSuccess ||
+          b < 1)
+        b = 1;
+      occc = b;
+    }
+    if (hipMemsetAsync(a.mbest, 0xff, sizeof(uint32_t) * tasks, st) != hipSuccess) return hipErrorUnknown;
+    const dim3 g((unsigned)(cus * occc)), gc(256);
+    unsigned *c = a.mcnt;
+    hipLaunchKernelGGL((mhrs_search<NT, 1, kMhrsK0>), g, dim3(kBlock), smc, st, a, 0u, nullptr, nullptr);
+    hipLaunchKernelGGL((mhrs_compact<NT>), gc, dim3(kBlock), 0, st, a, nullptr, nullptr, a.mq0, c + 0);
+    constexpr MhrsRound R1 = kMhrsRounds[0], R2 = kMhrsRounds[1], R3 = kMhrsRounds[2], R4 = kMhrsRounds[3],
+                        R5 = kMhrsRounds[4];
+    hipLaunchKernelGGL((mhrs_search<NT, R1.W, R1.K>), g, dim3(kBlock), smc, st, a, R1.A0, a.mq0, c + 0);
+    hipLaunchKernelGGL((mhrs_compact<NT>), gc, dim3(kBlock), 0, st, a, a.mq0, c + 0, a.mq1, c + 1);
+    hipLaunchKernelGGL((mhrs_search<NT, R2.W, R2.K>), g, dim3(kBlock), smc, st, a, R2.A0, a.mq1, c + 1);
+    hipLaunchKernelGGL((mhrs_compact<NT>), gc, dim3(kBlock), 0, st, a, a.mq1, c + 1, a.mq0, c + 2);
+    hipLaunchKernelGGL((mhrs_search<NT, R3.W, R3.K>), g, dim3(kBlock), smc, st, a, R3.A0, a.mq0, c + 2);
+    hipLaunchKernelGGL((mhrs_compact<NT>), gc, dim3(kBlock), 0, st, a, a.mq0, c + 2, a.mq1, c + 3);
+    hipLaunchKernelGGL((mhrs_search<NT, R4.W, R4.K>), g, dim3(kBlock), smc, st, a, R4.A0, a.mq1, c + 3);
+    hipLaunchKernelGGL((mhrs_compact<NT>), gc, dim3(kBlock), 0, st, a, a.mq1, c + 3, a.mq0, c + 4);
+    hipLaunchKernelGGL((mhrs_search<NT, R5.W, R5.K>), g, dim3(kBlock), smc, st, a, R5.A0, a.mq0, c + 4);
+  }
   return hipGetLastError();
 }
 
