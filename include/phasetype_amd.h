@@ -74,6 +74,17 @@ int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double *nu, const
                   const double *C, int zexp, int silent, const double *start, double *res, pht_reduce_fn reduce,
                   void *reduce_user, double *kernel_ms_total);
 
+/* Independent chains at once (no reference counterpart —
+ * the reference runs one chain per LJMA_Gibbs call, src/PHT_MCMC_Aslett.c:104):
+ * chain c on ctxs[c] (one context each, same n/method/mhit, observations set),
+ * its own host thread and R-compatible stream seeded by seeds[c]; chain c
+ * equals pht_gibbs_run after pht_set_seed(seeds[c]).  res: nchains blocks of
+ * it*m (pht_gibbs_run's layout); start: nchains*m values or start[0] < 0.
+ * Standalone builds only (fails inside R). */
+int pht_gibbs_run_chains(pht_ctx **ctxs, int nchains, const uint32_t *seeds, int it, int method, int m,
+                         const double *nu, const double *zeta, const int *T, const double *C, int zexp,
+                         const double *start, double *res, double *kernel_ms_max);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,7 +24,7 @@ import numpy as np
 
 from . import build as _build
 
-__all__ = ["load", "LJMA_Gibbs", "phtMCMC", "phtMCMC2", "Sweeper", "PhaseTypeError", "METHODS"]
+__all__ = ["load", "LJMA_Gibbs", "phtMCMC", "phtMCMC2", "Sweeper", "gibbs_chains", "PhaseTypeError", "METHODS"]
 
 METHODS = {"MHRS": 1, "ECS": 2, "DCS": 4}  # R/phtMCMC2.R:66-70
 
@@ -46,7 +46,7 @@ EXPORTS = [
     "LJMA_Gibbs", "R_init_PhaseType", "pht_last_error", "pht_device_count", "pht_bind_lapack", "pht_set_seed",
     "pht_unif_rand", "pht_rgamma", "pht_in_R", "pht_set_verbose", "pht_zexp", "pht_params_bytes", "pht_stats_len",
     "pht_build_params", "pht_ctx_create", "pht_ctx_destroy", "pht_ctx_set_obs", "pht_ctx_sweep",
-    "pht_ctx_sweep_debug", "pht_ctx_last_kernel_ms", "pht_gibbs_run",
+    "pht_ctx_sweep_debug", "pht_ctx_last_kernel_ms", "pht_gibbs_run", "pht_gibbs_run_chains",
 ]
 
 
@@ -95,6 +95,8 @@ def load(build_if_needed: bool = True) -> C.CDLL:
     L.pht_ctx_last_kernel_ms.argtypes = [C.c_void_p]
     L.pht_gibbs_run.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _dp, C.c_int, C.c_int,
                                 _dp, _dp, C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]
+    L.pht_gibbs_run_chains.argtypes = [C.POINTER(C.c_void_p), C.c_int, _up, C.c_int, C.c_int, C.c_int, _dp, _dp,
+                                       _ip, _dp, C.c_int, _dp, _dp, C.POINTER(C.c_double)]
     L.LJMA_Gibbs.argtypes = [_ip, _ip, _ip, _ip, _ip, _dp, _dp, _ip, _dp, _dp, _ip, _ip, _dp, _ip, _dp]
     p, pre = _lapack_path()
     if L.pht_bind_lapack(p.encode(), pre.encode()) != 0:
@@ -214,6 +216,37 @@ class Sweeper:
             self.close()
         except Exception:  # noqa: BLE001
             pass
+
+
+def gibbs_chains(seeds, y, censored, n, method, nu, zeta, T, C_, mhit: int = 1, it: int = 100, start=None,
+                 device: int = 0, obs0: int = 0):
+    """Independent Gibbs chains at once (pht_gibbs_run_chains):
+    chain c is the single chain of ``Sweeper.gibbs`` after ``set_seed(seeds[c])``.
+    Returns (draws [chains, it, m], max kernel ms)."""
+    L = load()
+    seeds = np.ascontiguousarray(seeds, np.uint32)
+    K, m = len(seeds), len(nu)
+    sws = []
+    try:
+        for _ in range(K):
+            sw = Sweeper(n, method, mhit, device=device)
+            sw.set_obs(y, censored, obs0=obs0)
+            sws.append(sw)
+        ctxs = (C.c_void_p * K)(*[sw.ctx for sw in sws])
+        res = np.zeros(K * it * m, np.float64)
+        st = np.array([-1.0]) if start is None else np.ascontiguousarray(start, np.float64).reshape(-1)
+        Tf = np.ascontiguousarray(np.asarray(T).reshape(-1, order="F"), np.int32)
+        Cf = np.ascontiguousarray(np.asarray(C_, np.float64).reshape(-1, order="F"))
+        kms = C.c_double(0.0)
+        zexp = zexp_for(y)
+        if L.pht_gibbs_run_chains(ctxs, K, seeds, it, method, m, np.ascontiguousarray(nu, np.float64),
+                                  np.ascontiguousarray(zeta, np.float64), Tf, Cf, zexp, st, res,
+                                  C.byref(kms)) != 0:
+            raise _err(L)
+        return res.reshape(K, m, it).transpose(0, 2, 1).copy(), kms.value
+    finally:
+        for sw in sws:
+            sw.close()
 
 
 def LJMA_Gibbs(it, mhit, method, n, m, nu, zeta, T, C_, y, l, censored, start, silent, res):

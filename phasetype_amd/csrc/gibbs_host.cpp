@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/phasetype_amd.h"
@@ -666,10 +667,10 @@ struct GibbsState {
   std::vector<double> TT, S, s;
   std::vector<std::vector<Ent>> Nl, Sl, sl, zl, TTl, Dl;
 
-  GibbsState(int it_, int n_, int m_, const double *nu_, const double *zeta_, const int *T, const double *C,
+  template <class Rng>
+  GibbsState(Rng &R, int it_, int n_, int m_, const double *nu_, const double *zeta_, const int *T, const double *C,
              const double *start, double *res_)
       : it(it_), n(n_), m(m_), n1(n_ + 1), nu(nu_), zeta(zeta_), res(res_) {
-    RHost &R = rhost();
     TT.assign(n1 * n1, 0.0);
     S.assign(n * n, 0.0);
     s.assign(n, 0.0);
@@ -711,8 +712,8 @@ struct GibbsState {
   }
 
   /* steps 4-5 (:340-397): compile statistics and draw from the posteriors */
-  void update(int iter, const double *z, const long long *Nt) {
-    RHost &R = rhost();
+  template <class Rng>
+  void update(Rng &R, int iter, const double *z, const long long *Nt) {
     std::vector<long long> Nsum(m, 0);
     std::vector<double> zsum(m, 0.0);
     for (int k = 0; k < m; k++) {
@@ -737,12 +738,13 @@ struct GibbsState {
 
 /* Run the Gibbs loop over a set of device shards; reduce = optional
  * cross-process all-reduce of the int64 statistics block. */
-int gibbs_run(int it, int mhit, int method, int n, int m, const double *nu, const double *zeta, const int *T,
+template <class Rng>
+int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *nu, const double *zeta, const int *T,
               const double *C, const double *y, long l, int silent, const double *start, double *res,
               std::vector<pht_ctx *> &ctxs, uint32_t k0, uint32_t k1, int zexp, pht_reduce_fn reduce,
               void *reduce_user, double *kernel_ms_total) {
   (void)y; (void)l; (void)mhit;
-  GibbsState G(it, n, m, nu, zeta, T, C, start, res);
+  GibbsState G(R, it, n, m, nu, zeta, T, C, start, res);
   const int disp = dispatch_method(method);
   const int sl = stats_len(n);
   std::vector<long long> tot(sl);
@@ -774,7 +776,7 @@ int gibbs_run(int it, int mhit, int method, int n, int m, const double *nu, cons
       return -1;
     }
     for (int k = 0; k < n; k++) z[k] = ldexp((double)tot[k], -zexp);
-    G.update(iter, z.data(), tot.data() + 2 * n);
+    G.update(R, iter, z.data(), tot.data() + 2 * n);
   }
   if (kernel_ms_total) *kernel_ms_total = kms;
   return 0;
@@ -797,10 +799,70 @@ extern "C" int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double
   const uint32_t k0 = (uint32_t)(R.u() * 4294967296.0);
   const uint32_t k1 = (uint32_t)(R.u() * 4294967296.0);
   std::vector<pht_ctx *> ctxs{c};
-  int rc = gibbs_run(it, c->mhit, method, c->n, m, nu, zeta, T, C, nullptr, c->count, silent, start, res, ctxs, k0,
+  int rc = gibbs_run(R, it, c->mhit, method, c->n, m, nu, zeta, T, C, nullptr, c->count, silent, start, res, ctxs, k0,
                      k1, zexp, reduce, reduce_user, kernel_ms_total);
   R.end();
   return rc;
+}
+
+/*
+ * Several independent chains at once: chain c runs on its
+ * own context (device buffers and HIP stream) from a host thread of its own,
+ * with its own R-compatible stream seeded by seeds[c] (standalone mode: the
+ * Gamma draws and the Philox key come from it), so chain c is exactly the
+ * single-chain pht_gibbs_run after pht_set_seed(seeds[c]).  At small N each
+ * chain's kernels leave most of the GPU idle (their time is the longest
+ * latent path); the chains' kernels run concurrently on their streams and the
+ * host setups overlap.  res is [chain][it x m] (each block as pht_gibbs_run);
+ * start is [chain][m] or start[0] < 0.  Not for use inside R (threads).
+ */
+namespace {
+struct OwnRng {
+  pht_rstream rs;
+  double u() { return pht_rs_unif_rand(&rs); }
+  double gamma(double a, double sc) { return pht_rs_rgamma(&rs, a, sc); }
+};
+}  // namespace
+
+extern "C" int pht_gibbs_run_chains(pht_ctx **ctxs, int nchains, const uint32_t *seeds, int it, int method, int m,
+                                    const double *nu, const double *zeta, const int *T, const double *C, int zexp,
+                                    const double *start, double *res, double *kernel_ms_max) {
+  if (nchains < 1 || !ctxs || !seeds) {
+    set_err("pht_gibbs_run_chains: need nchains >= 1 contexts and seeds");
+    return -1;
+  }
+  if (rhost().inR) {
+    set_err("pht_gibbs_run_chains is not available inside R (host threads)");
+    return -1;
+  }
+  std::vector<int> rc(nchains, 0);
+  std::vector<double> kms(nchains, 0.0);
+  std::vector<std::string> err(nchains);
+  std::vector<std::thread> th;
+  for (int c = 0; c < nchains; c++) {
+    th.emplace_back([&, c]() {
+      OwnRng R;
+      pht_rs_set_seed(&R.rs, seeds[c]);
+      const uint32_t k0 = (uint32_t)(R.u() * 4294967296.0);
+      const uint32_t k1 = (uint32_t)(R.u() * 4294967296.0);
+      std::vector<pht_ctx *> one{ctxs[c]};
+      const double *st = (start && start[0] >= 0) ? start + (size_t)c * m : start;
+      rc[c] = gibbs_run(R, it, ctxs[c]->mhit, method, ctxs[c]->n, m, nu, zeta, T, C, nullptr, ctxs[c]->count, 1,
+                        st, res + (size_t)c * it * m, one, k0, k1, zexp, nullptr, nullptr, &kms[c]);
+      if (rc[c]) err[c] = g_err;
+    });
+  }
+  for (auto &t : th) t.join();
+  double mx = 0.0;
+  for (int c = 0; c < nchains; c++) {
+    if (rc[c]) {
+      set_err("chain %d: %s", c, err[c].c_str());
+      return -1;
+    }
+    mx = std::max(mx, kms[c]);
+  }
+  if (kernel_ms_max) *kernel_ms_max = mx;
+  return 0;
 }
 
 /* ======================================================= .C entry point */
@@ -841,7 +903,7 @@ extern "C" void LJMA_Gibbs(int *it, int *mhit, int *method, int *n, int *m, doub
     if (pht_ctx_set_obs(c, y + lo, censored + lo, hi - lo, lo)) rc = -1;
   }
   if (rc == 0)
-    rc = gibbs_run(*it, *mhit, *method, *n, *m, nu, zeta, T, C, y, L, *silent, start, res, ctxs, k0, k1, zexp,
+    rc = gibbs_run(R, *it, *mhit, *method, *n, *m, nu, zeta, T, C, y, L, *silent, start, res, ctxs, k0, k1, zexp,
                    nullptr, nullptr, nullptr);
   for (pht_ctx *c : ctxs) pht_ctx_destroy(c);
   if (rc == 0) say("\n\nCompleted MCMC run, returning results ...\n");

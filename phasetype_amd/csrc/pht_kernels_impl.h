@@ -132,6 +132,11 @@ template <int NT, int W, int K>
 __global__ void __launch_bounds__(kBlock) mhrs_search(SweepArgs a, uint32_t A0, const uint32_t *qin,
                                                       const unsigned *cin) {
   extern __shared__ __align__(16) unsigned char smem[];
+  const int T1 = 1 + a.mhit;
+  const long total = (qin ? (long)(*cin) : a.count * T1) * W;
+  /* block b owns claim chunks b, b + grid, ...: none when b * 64 >= total
+   * (small shards, empty rounds): leave before staging anything */
+  if ((long)blockIdx.x * kClaimChunk >= total) return;
   const Par<NT> P = stage_params<NT>(a, (PHT_LDS unsigned char *)smem);
   /* items are claimed one at a time through an LDS cursor (claim_pos: the
    * block's 64-item chunks), so a lane whose item ends takes the next one
@@ -141,8 +146,6 @@ __global__ void __launch_bounds__(kBlock) mhrs_search(SweepArgs a, uint32_t A0, 
   pht_stage_math_tables();
   __syncthreads();
   const int n = P.n();
-  const int T1 = 1 + a.mhit;
-  const long total = (qin ? (long)(*cin) : a.count * T1) * W;
   long item = 0;
   /* item state */
   bool have = false;

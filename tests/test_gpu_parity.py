@@ -189,3 +189,25 @@ def test_longest_paths_bitexact(gpu, orc, monkeypatch, group):
         for f in ("B", "pre", "flags"):
             assert np.array_equal(g[f], o[f]), f
         assert np.array_equal(g["N"], o["N"])
+
+
+@pytest.mark.parametrize("method,n,cf", [(2, 5, 0.3), (1, 3, 0.3), (4, 3, 0.0)])
+def test_chains_equal_single_runs(gpu, method, n, cf):
+    """pht_gibbs_run_chains (independent chains on their own contexts,
+    streams and host threads): chain c is bit-identical to
+    the single chain run after set_seed(seeds[c])."""
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 3000, seed=77 + n, censor_frac=cf)
+    T, theta = bd_exit_structure(n)
+    nu, zeta = 1 + 50 * theta, np.full(len(theta), 50.0)
+    Cm = np.ones(T.shape)
+    seeds = [11, 22, 33, 44]
+    got, _ = P.gibbs_chains(seeds, y, cen, n, method, nu, zeta, T, Cm, it=6)
+    zexp = P.zexp_for(y)
+    sw = P.Sweeper(n, method, 1)
+    sw.set_obs(y, cen)
+    for c, sd in enumerate(seeds):
+        P.set_seed(sd)
+        want = sw.gibbs(6, method, nu, zeta, T, Cm, zexp)
+        assert np.array_equal(got[c], want), c
+    assert not np.array_equal(got[0], got[1])
