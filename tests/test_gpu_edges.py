@@ -1,0 +1,81 @@
+"""GPU edge cases, per observation against the oracle's device
+specification (oracle/pht_oracle_impl.h, ORC_DEV), bit for bit:
+empty and ragged shards (around the 64-lane wavefront and 256-lane block),
+one and two transient states, the runtime-n kernels at n = 32 (kMaxN),
+zero and tiny absorption times, all-censored data, mhit 0 and 3, and the
+multi-kernel MHRS search on a single observation."""
+import numpy as np
+import pytest
+
+import phasetype_amd as P
+from phasetype_amd.synth import bd_exit, simulate_ph
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("B", "pre", "flags", "ndraw", "zq", "N")
+
+
+def _check(orc, n, method, y, cen, mhit=1, key=(3, 5), sweep=2):
+    S, s = bd_exit(n)
+    y = np.ascontiguousarray(y, np.float64)
+    cen = np.ascontiguousarray(cen, np.int32)
+    zexp = int(orc.lib.orc_zexp(y, len(y))) if len(y) else 40
+    sw = P.Sweeper(n, method, mhit)
+    sw.set_obs(y, cen)
+    g = sw.sweep_debug(S, s, key=key, sweep=sweep, zexp=zexp)
+    st = sw.sweep(S, s, key=key, sweep=sweep, zexp=zexp)
+    sw.close()
+    L = 2 * n + n * n
+    if len(y) == 0:
+        assert not np.any(st[:L])
+        return
+    o = orc.dev_sweep(method, S, s, y, cen, mhit=mhit, key=key, sweep=sweep, zexp=zexp)
+    for f in FIELDS:
+        assert np.array_equal(g[f], o[f]), (f, n, method)
+    assert np.array_equal(st[:L], g["stats"][:L])
+
+
+@pytest.mark.parametrize("method", [1, 2, 4])
+@pytest.mark.parametrize("N", [0, 1, 63, 65, 257])
+def test_empty_and_ragged_shards(gpu, orc, method, N):
+    S, s = bd_exit(5)
+    y, cen = simulate_ph(S, s, N, seed=900 + N, censor_frac=0.3)
+    _check(orc, 5, method, y, cen)
+
+
+@pytest.mark.parametrize("method", [1, 2, 4])
+@pytest.mark.parametrize("n", [1, 2, 32])
+def test_state_counts(gpu, orc, method, n):
+    S, s = bd_exit(n)
+    N = 300 if n < 32 else 120
+    y, cen = simulate_ph(S, s, N, seed=1000 + n, censor_frac=0.3)
+    _check(orc, n, method, y, cen)
+
+
+@pytest.mark.parametrize("method", [1, 2, 4])
+def test_zero_and_tiny_times(gpu, orc, method):
+    y = np.array([0.0, 1e-300, 1e-12, 1e-6, 0.0, 2.5, 0.0, 1e-9])
+    cen = np.array([0, 0, 0, 0, 1, 0, 1, 1], np.int32)
+    _check(orc, 4, method, y, cen)
+
+
+@pytest.mark.parametrize("method", [1, 2])
+def test_all_censored(gpu, orc, method):
+    S, s = bd_exit(6)
+    y, _ = simulate_ph(S, s, 500, seed=77)
+    _check(orc, 6, method, y, np.ones(len(y), np.int32))
+
+
+@pytest.mark.parametrize("mhit", [0, 3])
+def test_mhrs_mhit(gpu, orc, mhit):
+    S, s = bd_exit(4)
+    y, cen = simulate_ph(S, s, 400, seed=31 + mhit, censor_frac=0.2)
+    _check(orc, 4, 1, y, cen, mhit=mhit)
+
+
+def test_mhrs_single_hard_observation(gpu, orc):
+    """One observation far in the tail (survival ~1e-4): its chains need
+    thousands of attempts, found by the wide search rounds."""
+    S, s = bd_exit(3)
+    y = np.array([9.0])
+    _check(orc, 3, 1, y, np.zeros(1, np.int32), mhit=2)
