@@ -27,7 +27,7 @@ SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = ["pht_device.h", "pht_env.h", "pht_kernels.h", "pht_kernels_impl.h", "pht_layout.h", "rstream.h",
            "pht_ecs_round.h", "pht_ecs_group.h"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
-DEFAULT_DEFINES: tuple = ("PHT_DETMATH_LDS", "PHT_ENV_K=9")
+DEFAULT_DEFINES: tuple = ("PHT_DETMATH_LDS",)
 
 
 def _hipcc() -> str:

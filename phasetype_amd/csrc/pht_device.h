@@ -517,225 +517,6 @@ __device__ __forceinline__ int arms(Env &e, const double xinit[4], double xl, do
   return arms_loop(e, f, xprev, yprev, xsamp, ln, 0);
 }
 
-/* ------------------------------------------------ register fast path */
-/* The freshly initialised envelope always has 9 points at fixed positions
- * (bound, 4 evaluated points, 4 intersections).  Env9 holds them in
- * registers: meet/cumulate/invert/Metropolis run with compile-time indices
- * (selects instead of LDS or scratch traffic), ey is computed once per point
- * in cumulate and reused by invert (same value: same expression, same
- * operands).  Only a rejected first proposal (an envelope update, ~10 % of
- * ECS sojourns) copies the points into a general envelope and continues in
- * arms_loop().  Every arithmetic step is the one of arms_meet /
- * arms_cumulate / arms_invert / arms_loop, so results are identical. */
-struct Env9 {
-  double x[9], y[9], cum[9], ymax;
-#ifndef PHT_ENV9_LEAN
-  double ey[9];
-#endif
-};
-
-template <int K>
-__device__ __forceinline__ void env9_meet(Env9 &e) {
-  constexpr int last = 8;
-  constexpr bool il = (K >= 3), ir = (K + 3 <= last), irl = (K >= 1 && K + 1 <= last);
-  double gl = 0.0, gr = 0.0, grl = 0.0, dl = 0.0, dr = 0.0;
-  double xm1 = 0.0, ym1 = 0.0, xp1 = 0.0, yp1 = 0.0;
-  if constexpr (K >= 1) { xm1 = e.x[K - 1]; ym1 = e.y[K - 1]; }
-  if constexpr (K + 1 <= last) { xp1 = e.x[K + 1]; yp1 = e.y[K + 1]; }
-  if constexpr (il) gl = PHT_DIV((ym1 - e.y[K - 3]), (xm1 - e.x[K - 3]));
-  if constexpr (ir) gr = PHT_DIV((yp1 - e.y[K + 3]), (xp1 - e.x[K + 3]));
-  if constexpr (irl) grl = PHT_DIV((yp1 - ym1), (xp1 - xm1));
-  if constexpr (irl && il) gl = (gl < grl) ? gl + (1.0 + 1.0) * (grl - gl) : gl;
-  if constexpr (irl && ir) gr = (gr > grl) ? gr + (1.0 + 1.0) * (grl - gr) : gr;
-  if constexpr (il && irl) {
-    dr = (gl - grl) * (xp1 - xm1);
-    dr = (dr < kYEps) ? kYEps : dr;
-  }
-  if constexpr (ir && irl) {
-    dl = (grl - gr) * (xp1 - xm1);
-    dl = (dl < kYEps) ? kYEps : dl;
-  }
-  if constexpr (il && ir && irl) {
-    e.x[K] = PHT_DIV((dl * xp1 + dr * xm1), (dl + dr));
-    e.y[K] = PHT_DIV((dl * yp1 + dr * ym1 + dl * dr), (dl + dr));
-  } else if constexpr (il && irl) {
-    e.x[K] = xp1;
-    e.y[K] = yp1 + dr;
-  } else if constexpr (ir && irl) {
-    e.x[K] = xm1;
-    e.y[K] = ym1 + dl;
-  } else if constexpr (il) {
-    e.y[K] = ym1 + gl * (e.x[K] - xm1);
-  } else if constexpr (ir) {
-    e.y[K] = yp1 - gr * (xp1 - e.x[K]);
-  }
-}
-
-__device__ __forceinline__ void env9_cumulate(Env9 &e) {
-  double ymax = e.y[0];
-#pragma unroll
-  for (int k = 1; k < 9; k++) ymax = (e.y[k] > ymax) ? e.y[k] : ymax;
-  e.ymax = ymax;
-#ifdef PHT_ENV9_LEAN
-  double ey[9];
-#else
-  double *ey = e.ey;
-#endif
-#pragma unroll
-  for (int k = 0; k < 9; k++) ey[k] = expshift(e.y[k], ymax);
-  double cum = 0.;
-  e.cum[0] = cum;
-#pragma unroll
-  for (int k = 1; k < 9; k++) {
-    const double xp = e.x[k - 1], xk = e.x[k], yp = e.y[k - 1], yk = e.y[k];
-    const double lin = 0.5 * (ey[k] + ey[k - 1]) * (xk - xp);
-    const double ex = (PHT_DIV((ey[k] - ey[k - 1]), (yk - yp))) * (xk - xp);
-    const double a = (xp == xk) ? 0. : ((fabs(yk - yp) < kYEps) ? lin : ex);
-    cum = cum + a;
-    e.cum[k] = cum;
-  }
-}
-
-/* arms_invert on Env9: the segment scan runs top-down with selects */
-__device__ __forceinline__ void env9_invert(const Env9 &e, double prob, WPt &p) {
-  const double u = prob * e.cum[8];
-  int q = 8;
-  double cl = e.cum[7], cr = e.cum[8];
-  double xl = e.x[7], xr = e.x[8], yl = e.y[7], yr = e.y[8];
-#ifndef PHT_ENV9_LEAN
-  double eyl = e.ey[7], eyr = e.ey[8];
-#endif
-  bool go = true;
-#pragma unroll
-  for (int k = 7; k >= 1; k--) {
-    go = go && (cl > u); /* cl == cum[k] here */
-    if (go) {
-      q = k;
-      cr = e.cum[k]; cl = e.cum[k - 1];
-      xr = e.x[k]; xl = e.x[k - 1];
-      yr = e.y[k]; yl = e.y[k - 1];
-#ifndef PHT_ENV9_LEAN
-      eyr = e.ey[k]; eyl = e.ey[k - 1];
-#endif
-    }
-  }
-#ifdef PHT_ENV9_LEAN
-  const double eyl = expshift(yl, e.ymax), eyr = expshift(yr, e.ymax);
-#endif
-  p.pr = q;
-  const double prop = PHT_DIV((u - cl), (cr - cl));
-  if (xl == xr) {
-    p.x = xr; p.y = yr; p.ey = eyr;
-    return;
-  }
-  if (fabs(yr - yl) < kYEps) {
-    if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
-      p.x = xl + (PHT_DIV((xr - xl), (eyr - eyl))) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
-    else
-      p.x = xl + (xr - xl) * prop;
-    p.ey = (PHT_DIV((p.x - xl), (xr - xl))) * (eyr - eyl) + eyl;
-    p.y = logshift(p.ey, e.ymax);
-  } else {
-    p.x = xl + (PHT_DIV((xr - xl), (yr - yl))) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
-    p.y = (PHT_DIV((p.x - xl), (xr - xl))) * (yr - yl) + yl;
-    p.ey = expshift(p.y, e.ymax);
-  }
-}
-
-/* arms() with the first iteration on Env9; `slow` is the general envelope
- * used only after a rejection.  Same draws, evaluations and results. */
-template <class Env, class F>
-__device__ __forceinline__ int arms_fast(Env &slow, const double xinit[4], double xl, double xr, F &f, double xprev,
-                                         double &xsamp, Lane &ln, ArmsPend *pend = nullptr) {
-  if ((xinit[0] <= xl) || (xinit[3] >= xr)) return 1003;
-  if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) return 1004;
-  Env9 e;
-  e.x[0] = xl;
-  e.y[0] = 0.0;
-  double yi[4];
-  if constexpr (F::kInit4) {
-    f.init4(xinit, yi);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; k++) yi[k] = f(xinit[k]);
-  }
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    e.x[2 * k + 1] = xinit[k];
-    e.y[2 * k + 1] = yi[k];
-    e.x[2 * k + 2] = 0.0;
-    e.y[2 * k + 2] = 0.0;
-  }
-  ln.neval += 4;
-  e.x[8] = xr;
-  env9_meet<0>(e);
-  env9_meet<2>(e);
-  env9_meet<4>(e);
-  env9_meet<6>(e);
-  env9_meet<8>(e);
-  env9_cumulate(e);
-  if ((xprev < xl) || (xprev > xr)) return 1007;
-  const double yprev = f(xprev);
-  ln.neval++;
-  PHT_STAMP(ln, 1);
-  /* iteration 0 (arms_loop body) */
-  WPt p;
-  env9_invert(e, dev_u(ln.r), p);
-  const double u = dev_u(ln.r) * p.ey;
-  const double yv = logshift(u, e.ymax);
-  const double ynew = f(p.x);
-  ln.neval++;
-  PHT_STAMP(ln, 5);
-  if (yv >= ynew) {
-    /* rejected: hand the envelope to the general code */
-    slow.cnt = 9;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      slow.sX(k, e.x[k]);
-      slow.sY(k, e.y[k]);
-      slow.sCUM(k, e.cum[k]);
-    }
-    slow.ymax = e.ymax;
-    p.y = ynew;
-    p.ey = expshift(p.y, e.ymax);
-    if (pend) { /* the caller continues with arms_step() */
-      pend->px = p.x; pend->py = p.y; pend->pey = p.ey; pend->pr = p.pr;
-      pend->yprev = yprev;
-      pend->it = 1;
-      return -1;
-    }
-    arms_update(slow, p, f, ln);
-    const int rc = arms_loop(slow, f, xprev, yprev, xsamp, ln, 1);
-    PHT_STAMP(ln, 4);
-    return rc;
-  }
-  /* Metropolis step: ql = first k with x[k+1] >= xprev */
-  int ql = 0;
-  double xql = e.x[0], yql = e.y[0], xqr = e.x[1], yqr = e.y[1];
-  bool go = true;
-#pragma unroll
-  for (int k = 1; k < 8; k++) {
-    go = go && (xqr < xprev); /* xqr == x[k] here */
-    if (go) {
-      ql = k;
-      xql = e.x[k]; yql = e.y[k];
-      xqr = e.x[k + 1]; yqr = e.y[k + 1];
-    }
-  }
-  (void)ql;
-  double w = PHT_DIV((xprev - xql), (xqr - xql));
-  double zold = yql + w * (yqr - yql);
-  double znew = p.y;
-  if (yprev < zold) zold = yprev;
-  if (ynew < znew) znew = ynew;
-  w = ynew - znew - yprev + zold;
-  if (w > 0.0) w = 0.0;
-  w = (w > -kYCeil) ? pht_exp_core(w) : 0.0;
-  const double um = dev_u(ln.r);
-  xsamp = (um > w) ? xprev : p.x;
-  return 0;
-}
-
 /* ====================================================== categorical scans */
 /* start state ~ pi (oracle: orcD_pistart) */
 template <int NT>
@@ -969,12 +750,11 @@ __device__ __forceinline__ EcsDens<NT> ecs_dens(const Par<NT> &P, EcsLane<NT> &s
   return ecs_dens(P, st, lam_max(P));
 }
 
-/* start of a non-absorbing jump: ARMS sojourn (:307-342).  With `pend`
- * non-null a rejected first proposal leaves the jump pending (false is
- * returned; continue with ecs_jump_resume); otherwise the jump completes. */
+/* one complete non-absorbing jump: ARMS sojourn (:307-342), moveMass and
+ * the categorical (ecs_jump_finish).  The persistent kernel runs the same
+ * steps in converged rounds (pht_ecs_round.h). */
 template <int NT, class Env, class Sink>
-__device__ __forceinline__ bool ecs_jump_start(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st,
-                                               ArmsPend *pend) {
+__device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st) {
   const int n = P.n();
   const double y_t = st.yt;
   if (!st.haveE0) { /* s_j = 0: no absorb test ran at this state */
@@ -989,34 +769,8 @@ __device__ __forceinline__ bool ecs_jump_start(const Par<NT> &P, Lane &ln, Env &
   xinit[2] = xinit[1] * 2.0;
   xinit[3] = y_t - xinit[0];
   double xsamp = 0.0;
-#ifdef PHT_ECS_NOFAST
-  (void)pend;
   const int ainfo = arms(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln);
-#else
-  const int ainfo = arms_fast(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln, pend);
-  if (ainfo == -1) return false;
-#endif
-  PHT_STAMP(ln, 2);
   ecs_jump_finish(P, ln, sk, st, f, xsamp, ainfo);
-  return true;
-}
-
-/* one ARMS step of a pending jump; true when the jump completed */
-template <int NT, class Env, class Sink>
-__device__ __forceinline__ bool ecs_jump_resume(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st,
-                                                ArmsPend &pend) {
-  EcsDens<NT> f = ecs_dens(P, st);
-  double xsamp = 0.0;
-  const int rc = arms_step(env, f, pend, 0.0, xsamp, ln);
-  if (rc == 1) return false;
-  ecs_jump_finish(P, ln, sk, st, f, xsamp, rc);
-  return true;
-}
-
-/* one complete non-absorbing jump */
-template <int NT, class Env, class Sink>
-__device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st) {
-  ecs_jump_start(P, ln, env, sk, st, nullptr);
 }
 
 template <int NT, class Env, class Sink>

@@ -8,12 +8,11 @@
  * from (y, ymax) where used (bit-identical).
  *
  * EnvPrivate  all 100 points in lane-private memory (scratch).
- * EnvLds<K>   the first K points in LDS, lane-interleaved (point k of lane t
- *             at base[k * stride + t], so a wavefront touching the same k
- *             reads 512 contiguous bytes: conflict-free ds_read_b64), points
- *             K..99 in private memory.  An ARMS call holds 9 points plus 2
- *             per rejection; K = 11 keeps one rejection in LDS, rarer calls
- *             spill.  Same results as EnvPrivate for any K.
+ * EnvLdsXY<K> x and y of the first K points in LDS, lane-interleaved (point
+ *             k of lane t at base[k * stride + t]: a wavefront touching
+ *             the same k reads 512 contiguous bytes, conflict-free
+ *             ds_read_b64); cum and points K..99 in private memory.  Same
+ *             results as EnvPrivate for any K.
  */
 #ifndef PHT_ENV_H
 #define PHT_ENV_H
@@ -41,36 +40,6 @@ struct EnvPrivate {
 #ifndef PHT_PRIV
 #define PHT_PRIV __attribute__((address_space(5)))
 #endif
-
-/* K points per lane in LDS (stride = threads per block), the rest in a
- * separate private spill array (kept out of this struct so that cnt, ymax
- * and the LDS base stay in registers). */
-template <int K, int STRIDE>
-struct EnvLds {
-  static constexpr int kSpill = 100 - K;
-  PHT_LDS double *l;  /* lane's element 0 */
-  PHT_PRIV double *ov; /* [3][kSpill] */
-  int cnt;
-  double ymax;
-  __device__ __forceinline__ void bind(PHT_LDS double *lds, int tid, PHT_PRIV double *spill) {
-    l = lds + tid;
-    ov = spill;
-  }
-  static constexpr int lds_doubles_per_lane() { return 3 * K; }
-  __device__ __forceinline__ double X(int k) const { if (k < K) return l[k * STRIDE]; return ov[k - K]; }
-  __device__ __forceinline__ double Y(int k) const { if (k < K) return l[(K + k) * STRIDE]; return ov[kSpill + k - K]; }
-  __device__ __forceinline__ double CUM(int k) const {
-    if (k < K) return l[(2 * K + k) * STRIDE];
-    return ov[2 * kSpill + k - K];
-  }
-  __device__ __forceinline__ void sX(int k, double v) { if (k < K) l[k * STRIDE] = v; else ov[k - K] = v; }
-  __device__ __forceinline__ void sY(int k, double v) {
-    if (k < K) l[(K + k) * STRIDE] = v; else ov[kSpill + k - K] = v;
-  }
-  __device__ __forceinline__ void sCUM(int k, double v) {
-    if (k < K) l[(2 * K + k) * STRIDE] = v; else ov[2 * kSpill + k - K] = v;
-  }
-};
 
 /* x and y of the first K points per lane in LDS (lane-interleaved), the
  * rest and all of cum in private memory.  The converged ECS round keeps cum

@@ -439,12 +439,8 @@ static hipError_t launch_persist(const SweepArgs &a, hipStream_t st) {
  * through an LDS cursor: a lane that finishes a path takes the
  * next observation at once, so the expensive ARMS phase runs with (almost)
  * all lanes of a wavefront active instead of waiting for the longest path.
- * The ARMS envelope lives in LDS (EnvLds<kEnvK>), lane-interleaved.
+ * The ARMS envelope's x/y live in LDS (EnvLdsXY), lane-interleaved.
  */
-#ifndef PHT_ENV_K
-#define PHT_ENV_K 11
-#endif
-constexpr int kEnvK = PHT_ENV_K;
 #ifndef PHT_SLOW_K
 #define PHT_SLOW_K 15
 #endif
@@ -484,11 +480,6 @@ ecs_exact_kernel(SweepArgs a) {
   P.d = (const PHT_LDS double *)lsm;
   P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
   P.Lr = L;
-#ifdef PHT_ECS_NOFAST
-  EnvLds<kEnvK, kBlock> env;
-  double spill[3 * EnvLds<kEnvK, kBlock>::kSpill];
-  env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill);
-#elif PHT_SLOW_K > 0
   /* the envelope's x and y in LDS (lane-interleaved) up to PHT_SLOW_K
    * points; cum lives in registers within a round (pht_ecs_round.h) and in
    * private memory for the general ARMS code */
@@ -496,10 +487,6 @@ ecs_exact_kernel(SweepArgs a) {
   double spill[2 * EnvLdsXY<PHT_SLOW_K, kBlock>::kSpill];
   double cumv[100];
   env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill, (PHT_PRIV double *)cumv);
-#else
-  (void)envl;
-  EnvPrivate env;
-#endif
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
   Lane ln;
 #ifdef PHT_STAMPS
@@ -618,16 +605,9 @@ ecs_exact_kernel(SweepArgs a) {
 #ifdef PHT_STAMPS
     ln.st_rounds++;
 #endif
-#if defined(PHT_ECS_NOFAST)
-    if (need) ecs_jump(P, ln, env, sk, st);
-#elif defined(PHT_ECS_PEND)
-    if (pend) pend = !ecs_jump_resume(P, ln, env, sk, st, pd);
-    if (need) pend = !ecs_jump_start(P, ln, env, sk, st, &pd);
-#else
     topup(need || pend);
     PHT_STAMP(ln, 12);
     ecs_round(P, ln, env, sk, st, need, pend, pd, lam);
-#endif
   }
 #ifdef PHT_STAMPS
   /* diagnostic builds: the extra words carry [rounds, 15 stamp slots] */
@@ -656,11 +636,7 @@ ecs_exact_kernel(SweepArgs a) {
 }
 
 static int smem_bytes_ecs(int n) {
-#ifdef PHT_ECS_NOFAST
-  return ((smem_bytes(n) + 4 + 15) & ~15) + EnvLds<kEnvK, kBlock>::lds_doubles_per_lane() * 8 * kBlock;
-#else
   return ((smem_bytes(n) + 4 + 15) & ~15) + 2 * PHT_SLOW_K * 8 * kBlock;
-#endif
 }
 
 template <int NT, bool DEBUG>

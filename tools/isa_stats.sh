@@ -9,7 +9,7 @@ OUT=${TMPDIR:-/tmp}/pht_isa
 mkdir -p "$OUT"
 cd "$OUT"
 /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -ffp-contract=off -Wno-pass-failed \
-  -DPHT_DETMATH_LDS -DPHT_ENV_K=9 "$@" -I"$ROOT/include" -I"$ROOT/phasetype_amd/csrc" \
+  -DPHT_DETMATH_LDS "$@" -I"$ROOT/include" -I"$ROOT/phasetype_amd/csrc" \
   --cuda-device-only -S -o k.s -DPHT_NT=${PHT_NT:-10} "$ROOT/phasetype_amd/csrc/pht_kernels_nt.hip"
 python3 - k.s <<'EOF'
 import re, sys, collections
