@@ -412,8 +412,15 @@ static int smem_bytes(int n) {
 /* persistent one-lane kernels: grid = CUs x occupancy, capped by the work */
 template <int NT, int METHOD, bool DEBUG>
 static hipError_t launch_persist(const SweepArgs &a, hipStream_t st) {
-  static int occ = -1, cus = 0;
+  static int occ = -1, cus = 0, lds_set = 0;
   const int sm = smem_bytes(a.n);
+  if (sm > lds_set) {
+    if (hipFuncSetAttribute((const void *)persist_kernel<NT, METHOD, DEBUG>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, sm) != hipSuccess)
+      return hipErrorUnknown;
+    lds_set = sm;
+    occ = -1;
+  }
   if (occ < 0) {
     int dev = 0;
     hipDeviceProp_t prop;
@@ -641,16 +648,21 @@ static int smem_bytes_ecs(int n) {
 
 template <int NT, bool DEBUG>
 static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
-  static int occ = -1, cus = 0;
+  static int occ = -1, cus = 0, lds_set = 0;
   const int sm = smem_bytes_ecs(a.n);
+  /* the runtime-n instantiation sees several n: raise the limit as needed */
+  if (sm > lds_set) {
+    if (hipFuncSetAttribute((const void *)ecs_exact_kernel<NT, DEBUG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            sm) != hipSuccess)
+      return hipErrorUnknown;
+    lds_set = sm;
+    occ = -1;
+  }
   if (occ < 0) {
     int dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
     cus = prop.multiProcessorCount;
-    if (hipFuncSetAttribute((const void *)ecs_exact_kernel<NT, DEBUG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            sm) != hipSuccess)
-      return hipErrorUnknown;
     int b = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, ecs_exact_kernel<NT, DEBUG>, kBlock, sm) != hipSuccess ||
         b < 1)
@@ -803,16 +815,20 @@ __global__ void __launch_bounds__(kBlock) ecs_group_kernel(SweepArgs a) {
 
 template <int NT, int G, bool DEBUG>
 static hipError_t launch_ecs_group(const SweepArgs &a, hipStream_t st) {
-  static int occ = -1, cus = 0;
+  static int occ = -1, cus = 0, lds_set = 0;
   const int sm = ((smem_bytes(a.n) + 4 + 15) & ~15) + (kBlock / G) * 5 * kGrpArr * 8;
+  if (sm > lds_set) {
+    if (hipFuncSetAttribute((const void *)ecs_group_kernel<NT, G, DEBUG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            sm) != hipSuccess)
+      return hipErrorUnknown;
+    lds_set = sm;
+    occ = -1;
+  }
   if (occ < 0) {
     int dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
     cus = prop.multiProcessorCount;
-    if (hipFuncSetAttribute((const void *)ecs_group_kernel<NT, G, DEBUG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            sm) != hipSuccess)
-      return hipErrorUnknown;
     int b = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, ecs_group_kernel<NT, G, DEBUG>, kBlock, sm) != hipSuccess ||
         b < 1)
