@@ -79,3 +79,24 @@ def test_mhrs_single_hard_observation(gpu, orc):
     S, s = bd_exit(3)
     y = np.array([9.0])
     _check(orc, 3, 1, y, np.zeros(1, np.int32), mhit=2)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_every_observation_processed(gpu, orc, n):
+    """Short paths (many absorb at their first test, so lanes idle on the
+    one-new-observation-per-round rule) over many shard sizes: the kernel's
+    observation counter equals N and every observation matches the oracle."""
+    S, s = bd_exit(n)
+    for N in (2, 5, 17, 64, 65, 130, 300, 1000, 5000):
+        y, cen = simulate_ph(S, s, N, seed=3 * N + n)
+        y = y * 0.05  # short absorption times: mostly zero-jump paths
+        sw = P.Sweeper(n, 2, 1)
+        sw.set_obs(y, cen)
+        zexp = int(orc.lib.orc_zexp(np.ascontiguousarray(y), len(y)))
+        st = sw.sweep(S, s, key=(8, N), sweep=1, zexp=zexp)
+        assert st[2 * n + n * n] == N, (N, st[2 * n + n * n])
+        g = sw.sweep_debug(S, s, key=(8, N), sweep=1, zexp=zexp)
+        o = orc.dev_sweep(2, S, s, y, cen, key=(8, N), sweep=1, zexp=zexp)
+        for f in FIELDS:
+            assert np.array_equal(g[f], o[f]), (N, f)
+        sw.close()
