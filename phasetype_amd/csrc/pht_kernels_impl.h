@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "pht_device.h"
 #include "pht_ecs_round.h"
 #include "pht_ecs_group.h"
@@ -409,29 +411,49 @@ static int smem_bytes(int n) {
   return L.bytes() + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4;
 }
 
-/* persistent one-lane kernels: grid = CUs x occupancy, capped by the work */
-template <int NT, int METHOD, bool DEBUG>
-static hipError_t launch_persist(const SweepArgs &a, hipStream_t st) {
-  static int occ = -1, cus = 0, lds_set = 0;
-  const int sm = smem_bytes(a.n);
-  if (sm > lds_set) {
-    if (hipFuncSetAttribute((const void *)persist_kernel<NT, METHOD, DEBUG>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, sm) != hipSuccess)
+/*
+ * Per-kernel launch configuration, shared by every host thread that
+ * launches the kernel (pht_gibbs_run_chains runs chains from several
+ * threads): the dynamic-LDS limit is raised whenever a larger footprint is
+ * launched (the runtime-n kernels see several n per process) and the
+ * occupancy is queried again after it; a mutex orders all of it.
+ */
+struct LaunchCfg {
+  std::mutex m;
+  int occ = -1, cus = 0, lds = 0, occ_sm = -1;
+};
+
+static hipError_t launch_config(LaunchCfg &cfg, const void *kernel, int sm, int *occ, int *cus) {
+  std::lock_guard<std::mutex> lock(cfg.m);
+  if (sm > cfg.lds) {
+    if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, sm) != hipSuccess)
       return hipErrorUnknown;
-    lds_set = sm;
-    occ = -1;
+    cfg.lds = sm;
   }
-  if (occ < 0) {
+  if (cfg.occ < 0 || sm != cfg.occ_sm) {
+    cfg.occ_sm = sm;
     int dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
-    cus = prop.multiProcessorCount;
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, persist_kernel<NT, METHOD, DEBUG>, kBlock, sm) != hipSuccess ||
-        b < 1)
-      b = 1;
-    occ = b;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kBlock, sm) != hipSuccess || b < 1) b = 1;
+    cfg.cus = prop.multiProcessorCount;
+    cfg.occ = b;
   }
+  *occ = cfg.occ;
+  *cus = cfg.cus;
+  return hipSuccess;
+}
+
+/* persistent one-lane kernels: grid = CUs x occupancy, capped by the work */
+template <int NT, int METHOD, bool DEBUG>
+static hipError_t launch_persist(const SweepArgs &a, hipStream_t st) {
+  static LaunchCfg cfg;
+  const int sm = smem_bytes(a.n);
+  int occ = 0, cus = 0;
+  if (hipError_t e = launch_config(cfg, (const void *)persist_kernel<NT, METHOD, DEBUG>, sm, &occ, &cus);
+      e != hipSuccess)
+    return e;
   long grid = (long)cus * occ;
   const long want = (a.count + kBlock - 1) / kBlock;
   if (grid > want) grid = want;
@@ -648,27 +670,11 @@ static int smem_bytes_ecs(int n) {
 
 template <int NT, bool DEBUG>
 static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
-  static int occ = -1, cus = 0, lds_set = 0;
+  static LaunchCfg cfg;
   const int sm = smem_bytes_ecs(a.n);
-  /* the runtime-n instantiation sees several n: raise the limit as needed */
-  if (sm > lds_set) {
-    if (hipFuncSetAttribute((const void *)ecs_exact_kernel<NT, DEBUG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            sm) != hipSuccess)
-      return hipErrorUnknown;
-    lds_set = sm;
-    occ = -1;
-  }
-  if (occ < 0) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
-    cus = prop.multiProcessorCount;
-    int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, ecs_exact_kernel<NT, DEBUG>, kBlock, sm) != hipSuccess ||
-        b < 1)
-      b = 1;
-    occ = b;
-  }
+  int occ = 0, cus = 0;
+  if (hipError_t e = launch_config(cfg, (const void *)ecs_exact_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
+    return e;
   long want = (a.count + kBlock - 1) / kBlock;
   /* blocks per CU: the occupancy limit, or fewer (a.occ) when the shard is
    * small and the longest paths, not throughput, set the time */
@@ -815,26 +821,12 @@ __global__ void __launch_bounds__(kBlock) ecs_group_kernel(SweepArgs a) {
 
 template <int NT, int G, bool DEBUG>
 static hipError_t launch_ecs_group(const SweepArgs &a, hipStream_t st) {
-  static int occ = -1, cus = 0, lds_set = 0;
+  static LaunchCfg cfg;
   const int sm = ((smem_bytes(a.n) + 4 + 15) & ~15) + (kBlock / G) * 5 * kGrpArr * 8;
-  if (sm > lds_set) {
-    if (hipFuncSetAttribute((const void *)ecs_group_kernel<NT, G, DEBUG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            sm) != hipSuccess)
-      return hipErrorUnknown;
-    lds_set = sm;
-    occ = -1;
-  }
-  if (occ < 0) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
-    cus = prop.multiProcessorCount;
-    int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, ecs_group_kernel<NT, G, DEBUG>, kBlock, sm) != hipSuccess ||
-        b < 1)
-      b = 1;
-    occ = b;
-  }
+  int occ = 0, cus = 0;
+  if (hipError_t e = launch_config(cfg, (const void *)ecs_group_kernel<NT, G, DEBUG>, sm, &occ, &cus);
+      e != hipSuccess)
+    return e;
   long want = (a.count + (kBlock / G) - 1) / (kBlock / G);
   long grid = (long)cus * occ;
   if (grid > want) grid = want;
@@ -847,13 +839,6 @@ static hipError_t launch_ecs_group(const SweepArgs &a, hipStream_t st) {
  * multi-wavefront rounds); queue counts stay on the device (no host sync) */
 template <int NT>
 static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
-    cus = prop.multiProcessorCount;
-  }
   if (a.mbest == nullptr || a.mq0 == nullptr || a.mq1 == nullptr || a.mcnt == nullptr || a.begin != 0)
     return hipErrorInvalidValue;
   const int sm = make_layout(a.n).bytes();
@@ -862,15 +847,13 @@ static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
   {
     const int smc = sm + 16; /* + the claim cursor */
     /* persistent grid: exactly the resident blocks (a block that started
-     * late would still own its share of the claim chunks) */
-    static int occc = -1;
-    if (occc < 0) {
-      int b = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, mhrs_search<NT, 1, kMhrsK0>, kBlock, smc) != hipSuccess ||
-          b < 1)
-        b = 1;
-      occc = b;
-    }
+     * late would still own its share of the claim chunks); the rounds'
+     * instantiations share one resource footprint */
+    static LaunchCfg cfg;
+    int occc = 0, cus = 0;
+    if (hipError_t e = launch_config(cfg, (const void *)mhrs_search<NT, 1, kMhrsK0>, smc, &occc, &cus);
+        e != hipSuccess)
+      return e;
     if (hipMemsetAsync(a.mbest, 0xff, sizeof(uint32_t) * tasks, st) != hipSuccess) return hipErrorUnknown;
     const dim3 g((unsigned)(cus * occc)), gc(256);
     unsigned *c = a.mcnt;
