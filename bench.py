@@ -104,7 +104,12 @@ def main():
     # share devices round-robin, the statistics travel through host memory).
     backend = os.environ.get("PHT_DIST_BACKEND", "nccl")
     coll_dev = "cpu"
-    if world > 1:
+    # Under torchrun (WORLD_SIZE set) the process group is initialised even at
+    # world 1, so `--nproc-per-node 1` runs the same RCCL code as N > 1.
+    # torch initialises the device BEFORE the library loads: the library then
+    # shares torch's HIP runtime (loaded the other way round, two runtimes are
+    # mapped and torch's sees no device).
+    if "WORLD_SIZE" in os.environ:
         import torch
         import torch.distributed as dist
 

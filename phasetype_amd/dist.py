@@ -30,13 +30,24 @@ def make_stats_allreduce(dist, n_words: int, device: str = "cpu"):
     import torch
 
     buf = torch.zeros(n_words, dtype=torch.int64, device=device)
+    on_gpu = buf.device.type == "cuda"
+    # GPU staging goes through one pinned host block: both copies are DMA
+    # from page-locked memory, and only one stream sync per sweep.
+    host = torch.zeros(n_words, dtype=torch.int64, pin_memory=on_gpu)
+    host_np = host.numpy()
 
     def reduce(arr: np.ndarray) -> None:
         if arr.dtype != np.int64 or arr.shape != (n_words,):
             raise ValueError(f"stats block must be int64[{n_words}], got {arr.dtype}{arr.shape}")
-        buf.copy_(torch.from_numpy(arr))
-        dist.all_reduce(buf)
-        arr[:] = buf.cpu().numpy()
+        host_np[:] = arr
+        if on_gpu:
+            buf.copy_(host, non_blocking=True)
+            dist.all_reduce(buf)
+            host.copy_(buf, non_blocking=True)
+            torch.cuda.current_stream(buf.device).synchronize()
+        else:
+            dist.all_reduce(host)
+        arr[:] = host_np
 
     return reduce
 
