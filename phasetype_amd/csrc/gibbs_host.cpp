@@ -27,6 +27,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -354,7 +356,163 @@ struct pht_ctx {
   long dbg_cap = 0;
   float last_ms = 0.f;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  struct ChainGroup *grp = nullptr; /* pht_gibbs_run_chains: exact ECS launched with the other chains */
+  int gidx = -1;
 };
+
+/* lanes of the persistent ECS grid on an MI355X (256 CUs x 2 blocks x 256) */
+constexpr long kSpreadLanes = 256L * 2 * 256;
+
+/*
+ * Chains whose sweeps go out together (pht_gibbs_run_chains, SURVEY.md
+ * §8f.4).  Each chain's thread builds its parameters into its slot of one
+ * pinned block and arrives; the last chain to arrive enqueues the whole sweep
+ * of every arrived chain on the group's stream: one parameter upload, one
+ * statistics reset, the censored-range kernels, ONE ecs_chains_kernel launch
+ * over all exact ranges, one statistics download.  The others wait for that
+ * sweep's `done` event.  A chain that stops (end of run or error) leaves the
+ * group, so the others never wait for it.
+ */
+struct ChainGroup {
+  int K = 0, device = 0, n = 0, pb = 0, sl = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int active = 0;
+  unsigned long gen = 0;
+  int rc = 0;
+  float ms = 0.f;
+  std::vector<int> who;          /* chains arrived for the pending sweep */
+  std::vector<SweepArgs> ex, ce; /* [K] exact / censored range arguments */
+  unsigned char *h_params = nullptr, *d_params = nullptr;  /* [K][pb] */
+  unsigned long long *h_stats = nullptr, *d_stats = nullptr; /* [K][sl] */
+  SweepArgs *h_args = nullptr, *d_args = nullptr;           /* [K] packed */
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+  hipStream_t stream = nullptr;
+};
+
+static void group_destroy(ChainGroup *g) {
+  if (!g) return;
+  (void)hipSetDevice(g->device);
+  if (g->stream) (void)hipStreamSynchronize(g->stream);
+  for (hipEvent_t e : {g->ev0, g->ev1, g->done})
+    if (e) (void)hipEventDestroy(e);
+  if (g->stream) (void)hipStreamDestroy(g->stream);
+  if (g->h_params) (void)hipHostFree(g->h_params);
+  if (g->h_stats) (void)hipHostFree(g->h_stats);
+  if (g->h_args) (void)hipHostFree(g->h_args);
+  if (g->d_params) (void)hipFree(g->d_params);
+  if (g->d_stats) (void)hipFree(g->d_stats);
+  if (g->d_args) (void)hipFree(g->d_args);
+  delete g;
+}
+
+static ChainGroup *group_create(int device, int K, int n) {
+  ChainGroup *g = new ChainGroup();
+  g->K = K;
+  g->device = device;
+  g->n = n;
+  g->pb = make_layout(n).bytes();
+  g->sl = stats_len(n);
+  g->active = K;
+  g->ex.resize(K);
+  g->ce.resize(K);
+  const size_t P = (size_t)g->pb * K, Sb = sizeof(unsigned long long) * g->sl * K, A = sizeof(SweepArgs) * K;
+  const bool ok = hipSetDevice(device) == hipSuccess &&
+                  hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) == hipSuccess &&
+                  hipEventCreate(&g->ev0) == hipSuccess && hipEventCreate(&g->ev1) == hipSuccess &&
+                  hipEventCreateWithFlags(&g->done, hipEventDisableTiming) == hipSuccess &&
+                  hipHostMalloc(&g->h_params, P, 0) == hipSuccess && hipMalloc(&g->d_params, P) == hipSuccess &&
+                  hipHostMalloc(&g->h_stats, Sb, 0) == hipSuccess && hipMalloc(&g->d_stats, Sb) == hipSuccess &&
+                  hipHostMalloc(&g->h_args, A, 0) == hipSuccess && hipMalloc(&g->d_args, A) == hipSuccess;
+  if (!ok) {
+    group_destroy(g);
+    return nullptr;
+  }
+  return g;
+}
+
+/* with g->m held: enqueue the sweep of the arrived chains and release them */
+static void group_fire(ChainGroup *g) {
+  const int k = (int)g->who.size();
+  hipError_t e = hipSetDevice(g->device);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(g->d_params, g->h_params, (size_t)g->pb * g->K, hipMemcpyHostToDevice, g->stream);
+  if (e == hipSuccess)
+    e = hipMemsetAsync(g->d_stats, 0, sizeof(unsigned long long) * g->sl * g->K, g->stream);
+  if (e == hipSuccess) e = hipEventRecord(g->ev0, g->stream);
+  int nx = 0;
+  for (int i = 0; i < k && e == hipSuccess; i++) {
+    const int w = g->who[i];
+    if (g->ce[w].count > 0) e = pht_launch_sweep(&g->ce[w], kMethodECS, 0, g->stream);
+    if (g->ex[w].count > 0) g->h_args[nx++] = g->ex[w];
+  }
+  if (e == hipSuccess && nx > 0)
+    e = hipMemcpyAsync(g->d_args, g->h_args, sizeof(SweepArgs) * nx, hipMemcpyHostToDevice, g->stream);
+  if (e == hipSuccess && nx > 0) e = pht_launch_ecs_chains(g->h_args, g->d_args, nx, g->stream);
+  if (e == hipSuccess) e = hipEventRecord(g->ev1, g->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(g->h_stats, g->d_stats, sizeof(unsigned long long) * g->sl * g->K, hipMemcpyDeviceToHost,
+                       g->stream);
+  if (e == hipSuccess) e = hipEventRecord(g->done, g->stream);
+  g->rc = (e == hipSuccess) ? 0 : (int)e;
+  g->who.clear();
+  g->gen++;
+  g->cv.notify_all();
+}
+
+/* chain c's sweep (parameters in c->h_params): returns when the group's sweep
+ * is done, with c->h_stats and c->last_ms filled */
+static int group_sweep(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int zexp) {
+  ChainGroup *g = c->grp;
+  const int w = c->gidx;
+  unsigned char *dp = g->d_params + (size_t)g->pb * w;
+  unsigned long long *ds = g->d_stats + (size_t)g->sl * w;
+  SweepArgs a;
+  memset(&a, 0, sizeof a);
+  a.params = dp;
+  a.n = c->n;
+  a.mhit = c->mhit;
+  a.y = c->d_y;
+  a.gid = c->d_gid;
+  a.k0 = k0;
+  a.k1 = k1;
+  a.sweep = sweep;
+  a.zscale = ldexp(1.0, zexp);
+  a.stats = ds;
+  SweepArgs ae = a;
+  ae.begin = 0;
+  ae.count = c->n_exact;
+  ae.newcap = getenv("PHT_NEWCAP") ? atoi(getenv("PHT_NEWCAP")) : 1;
+  ae.spread = getenv("PHT_SPREAD") ? atoi(getenv("PHT_SPREAD")) : (c->n_exact <= 2 * kSpreadLanes);
+  SweepArgs ac = a;
+  ac.cens = c->d_cens;
+  ac.begin = c->n_exact;
+  ac.count = c->count - c->n_exact;
+  std::unique_lock<std::mutex> lk(g->m);
+  memcpy(g->h_params + (size_t)g->pb * w, c->h_params, g->pb);
+  g->ex[w] = ae;
+  g->ce[w] = ac;
+  g->who.push_back(w);
+  const unsigned long my = g->gen;
+  if ((int)g->who.size() == g->active) group_fire(g);
+  else g->cv.wait(lk, [&] { return g->gen != my; });
+  const int rc = g->rc; /* the next sweep needs this chain's arrival: rc is still ours */
+  lk.unlock();
+  if (rc) {
+    set_err("chains sweep enqueue failed (%s)", hipGetErrorString((hipError_t)rc));
+    return -1;
+  }
+  HIPCHK(hipEventSynchronize(g->done));
+  HIPCHK(hipEventElapsedTime(&c->last_ms, g->ev0, g->ev1));
+  memcpy(c->h_stats, g->h_stats + (size_t)g->sl * w, sizeof(unsigned long long) * g->sl);
+  return 0;
+}
+
+static void group_leave(ChainGroup *g) {
+  std::lock_guard<std::mutex> lk(g->m);
+  g->active--;
+  if (!g->who.empty() && (int)g->who.size() == g->active) group_fire(g);
+}
 
 static void ctx_free_obs(pht_ctx *c) {
   (void)hipSetDevice(c->device);
@@ -504,8 +662,6 @@ static int exact_group(const pht_ctx *c) {
   return 0;
 }
 
-/* lanes of the persistent ECS grid on an MI355X (256 CUs x 2 blocks x 256) */
-constexpr long kSpreadLanes = 256L * 2 * 256;
 
 /* blocks per CU for the persistent ECS kernel (PHT_ECS_OCC forces it) */
 static int exact_occ(const pht_ctx *c) {
@@ -763,11 +919,15 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
     if (info < 0) return -1;
     for (pht_ctx *c : ctxs) {
       memcpy(c->h_params, pb.data(), pb.size());
-      if (ctx_enqueue(c, k0, k1, (uint32_t)iter, zexp, false)) return -1;
+      if (c->grp) {
+        if (group_sweep(c, k0, k1, (uint32_t)iter, zexp)) return -1;
+      } else if (ctx_enqueue(c, k0, k1, (uint32_t)iter, zexp, false)) {
+        return -1;
+      }
     }
     std::fill(tot.begin(), tot.end(), 0LL);
     for (pht_ctx *c : ctxs) {
-      if (ctx_wait(c)) return -1;
+      if (!c->grp && ctx_wait(c)) return -1;
       kms += c->last_ms;
       for (int k = 0; k < sl; k++) tot[k] += (long long)c->h_stats[k];
     }
@@ -835,6 +995,28 @@ extern "C" int pht_gibbs_run_chains(pht_ctx **ctxs, int nchains, const uint32_t 
     set_err("pht_gibbs_run_chains is not available inside R (host threads)");
     return -1;
   }
+  /* exact ECS ranges of all chains in one launch per sweep, when the chains
+   * share a device and n (PHT_CHAINS_LAUNCH=streams: one launch per chain) */
+  ChainGroup *grp = nullptr;
+  {
+    bool one = nchains >= 2;
+    for (int c = 0; c < nchains && one; c++)
+      one = ctxs[c]->method == kMethodECS && ctxs[c]->device == ctxs[0]->device && ctxs[c]->n == ctxs[0]->n &&
+            !ctxs[c]->grp;
+    const char *ev = getenv("PHT_CHAINS_LAUNCH");
+    if (ev && !strcmp(ev, "streams")) one = false;
+    if (one) {
+      grp = group_create(ctxs[0]->device, nchains, ctxs[0]->n);
+      if (!grp) {
+        set_err("pht_gibbs_run_chains: HIP allocation failed");
+        return -1;
+      }
+      for (int c = 0; c < nchains; c++) {
+        ctxs[c]->grp = grp;
+        ctxs[c]->gidx = c;
+      }
+    }
+  }
   std::vector<int> rc(nchains, 0);
   std::vector<double> kms(nchains, 0.0);
   std::vector<std::string> err(nchains);
@@ -850,9 +1032,17 @@ extern "C" int pht_gibbs_run_chains(pht_ctx **ctxs, int nchains, const uint32_t 
       rc[c] = gibbs_run(R, it, ctxs[c]->mhit, method, ctxs[c]->n, m, nu, zeta, T, C, nullptr, ctxs[c]->count, 1,
                         st, res + (size_t)c * it * m, one, k0, k1, zexp, nullptr, nullptr, &kms[c]);
       if (rc[c]) err[c] = g_err;
+      if (grp) group_leave(grp);
     });
   }
   for (auto &t : th) t.join();
+  if (grp) {
+    for (int c = 0; c < nchains; c++) {
+      ctxs[c]->grp = nullptr;
+      ctxs[c]->gidx = -1;
+    }
+    group_destroy(grp);
+  }
   double mx = 0.0;
   for (int c = 0; c < nchains; c++) {
     if (rc[c]) {

@@ -9,7 +9,9 @@
 #include "pht_layout.h"
 
 #define PHT_DECL(K) \
-  extern "C" hipError_t pht_launch_nt_##K(const pht::SweepArgs *a, int method, int debug, hipStream_t st);
+  extern "C" hipError_t pht_launch_nt_##K(const pht::SweepArgs *a, int method, int debug, hipStream_t st); \
+  extern "C" hipError_t pht_launch_chains_nt_##K(const pht::SweepArgs *h, const pht::SweepArgs *d, int nch, \
+                                                 hipStream_t st);
 PHT_DECL(0)
 PHT_DECL(3)
 PHT_DECL(5)
@@ -29,5 +31,25 @@ extern "C" hipError_t pht_launch_sweep(const pht::SweepArgs *a, int method, int 
     case 15: return pht_launch_nt_15(a, method, debug, st);
     case 20: return pht_launch_nt_20(a, method, debug, st);
     default: return pht_launch_nt_0(a, method, debug, st);
+  }
+}
+
+/* K chains' exact ECS ranges in one launch (h on the host, the same K
+ * SweepArgs already copied to d on the device, in stream order before the
+ * launch); the chains must share n.  See ecs_chains_kernel. */
+extern "C" hipError_t pht_launch_ecs_chains(const pht::SweepArgs *h, const pht::SweepArgs *d, int K, hipStream_t st) {
+  using namespace pht;
+  if (K < 1) return hipErrorInvalidValue;
+  const int n = h[0].n;
+  if (n < 1 || n > kMaxN || (make_layout(n).bytes() & 15) != 0) return hipErrorInvalidValue;
+  for (int c = 0; c < K; c++)
+    if (h[c].n != n || h[c].cens != nullptr || h[c].group > 1 || h[c].dbg_zq != nullptr) return hipErrorInvalidValue;
+  switch (n) {
+    case 3: return pht_launch_chains_nt_3(h, d, K, st);
+    case 5: return pht_launch_chains_nt_5(h, d, K, st);
+    case 10: return pht_launch_chains_nt_10(h, d, K, st);
+    case 15: return pht_launch_chains_nt_15(h, d, K, st);
+    case 20: return pht_launch_chains_nt_20(h, d, K, st);
+    default: return pht_launch_chains_nt_0(h, d, K, st);
   }
 }

@@ -48,5 +48,6 @@ struct SweepArgs {
 }  // namespace pht
 
 extern "C" hipError_t pht_launch_sweep(const pht::SweepArgs *a, int method, int debug, hipStream_t st);
+extern "C" hipError_t pht_launch_ecs_chains(const pht::SweepArgs *h, const pht::SweepArgs *d, int K, hipStream_t st);
 
 #endif

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <mutex>
 
 #include "pht_device.h"
@@ -73,9 +74,10 @@ __device__ __forceinline__ int nval(int n) { return NT > 0 ? NT : n; }
  * (the sorted order is walked by all blocks together; a wavefront's claims
  * are contiguous, so its y/gid loads coalesce).  Increasing in t. */
 constexpr int kClaimChunk = 64;
-__device__ __forceinline__ long claim_pos(long t) {
-  return ((t / kClaimChunk) * (long)gridDim.x + blockIdx.x) * kClaimChunk + (t % kClaimChunk);
+__device__ __forceinline__ long claim_pos(long t, unsigned blk, unsigned nblk) {
+  return ((t / kClaimChunk) * (long)nblk + blk) * kClaimChunk + (t % kClaimChunk);
 }
+__device__ __forceinline__ long claim_pos(long t) { return claim_pos(t, blockIdx.x, gridDim.x); }
 
 /* ================================================================ MHRS */
 /*
@@ -477,12 +479,10 @@ static hipError_t launch_persist(const SweepArgs &a, hipStream_t st) {
 #ifndef PHT_ECS_WAVES
 #define PHT_ECS_WAVES 0
 #endif
+/* blk / nblk: the block's index and the block count of its chain's grid
+ * (blockIdx.x / gridDim.x, except in ecs_chains_kernel) */
 template <int NT, bool DEBUG>
-__global__ void __launch_bounds__(kBlock)
-#if PHT_ECS_WAVES > 0
-__attribute__((amdgpu_waves_per_eu(PHT_ECS_WAVES, PHT_ECS_WAVES)))
-#endif
-ecs_exact_kernel(SweepArgs a) {
+__device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
   const Layout L = make_layout(n);
@@ -534,8 +534,8 @@ ecs_exact_kernel(SweepArgs a) {
      * wavefronts, so the longest paths (the first positions) go one per
      * wavefront instead of 64 to wavefront 0 */
     if (a.spread && t < kBlock)
-      return (long)(t & 63) * ((long)gridDim.x * (kBlock / 64)) + (long)(t >> 6) * gridDim.x + blockIdx.x;
-    return claim_pos(t);
+      return (long)(t & 63) * ((long)nblk * (kBlock / 64)) + (long)(t >> 6) * nblk + blk;
+    return claim_pos(t, blk, nblk);
   };
   long nextp = claim();
   double ny = 0.0;
@@ -664,6 +664,32 @@ ecs_exact_kernel(SweepArgs a) {
     if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
 }
 
+template <int NT, bool DEBUG>
+__global__ void __launch_bounds__(kBlock)
+#if PHT_ECS_WAVES > 0
+__attribute__((amdgpu_waves_per_eu(PHT_ECS_WAVES, PHT_ECS_WAVES)))
+#endif
+ecs_exact_kernel(SweepArgs a) {
+  ecs_exact_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
+}
+
+/*
+ * K independent chains' exact ECS observations in ONE launch (SURVEY.md
+ * §8f.4): block b serves chain b % K as its block b / K of nblk, staging that
+ * chain's parameters and adding into that chain's statistics.  An
+ * observation's result depends only on (its id, the chain's key, sweep and
+ * parameters), so every chain equals its own single launch bit for bit.
+ */
+template <int NT>
+__global__ void __launch_bounds__(kBlock)
+#if PHT_ECS_WAVES > 0
+__attribute__((amdgpu_waves_per_eu(PHT_ECS_WAVES, PHT_ECS_WAVES)))
+#endif
+ecs_chains_kernel(const SweepArgs *args, int K, unsigned nblk) {
+  const SweepArgs a = args[blockIdx.x % (unsigned)K];
+  ecs_exact_body<NT, false>(a, blockIdx.x / (unsigned)K, nblk);
+}
+
 static int smem_bytes_ecs(int n) {
   return ((smem_bytes(n) + 4 + 15) & ~15) + 2 * PHT_SLOW_K * 8 * kBlock;
 }
@@ -683,6 +709,24 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
   if (grid > want) grid = want;
   if (grid < 1) return hipSuccess;
   hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
+  return hipGetLastError();
+}
+
+/* h: the chains' arguments on the host (sizing), d: the same on the device */
+template <int NT>
+static hipError_t launch_ecs_chains(const SweepArgs *h, const SweepArgs *d, int K, hipStream_t st) {
+  static LaunchCfg cfg;
+  const int sm = smem_bytes_ecs(h[0].n);
+  int occ = 0, cus = 0;
+  if (hipError_t e = launch_config(cfg, (const void *)ecs_chains_kernel<NT>, sm, &occ, &cus); e != hipSuccess)
+    return e;
+  long want = 0;
+  for (int c = 0; c < K; c++) want = std::max(want, (h[c].count + kBlock - 1) / kBlock);
+  /* every chain gets the same share of the resident grid (at least one block) */
+  long nblk = std::max(1L, (long)cus * occ / K);
+  if (nblk > want) nblk = want;
+  if (nblk < 1) return hipSuccess;
+  hipLaunchKernelGGL((ecs_chains_kernel<NT>), dim3((unsigned)(nblk * K)), dim3(kBlock), sm, st, d, K, (unsigned)nblk);
   return hipGetLastError();
 }
 

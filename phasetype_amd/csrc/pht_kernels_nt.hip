@@ -16,3 +16,8 @@ extern "C" hipError_t PHT_CAT(pht_launch_nt_, PHT_NT)(const pht::SweepArgs *a, i
                                                      hipStream_t st) {
   return pht::launch_nt<PHT_NT>(*a, method, debug != 0, st);
 }
+
+extern "C" hipError_t PHT_CAT(pht_launch_chains_nt_, PHT_NT)(const pht::SweepArgs *h, const pht::SweepArgs *d, int K,
+                                                            hipStream_t st) {
+  return pht::launch_ecs_chains<PHT_NT>(h, d, K, st);
+}

@@ -191,11 +191,18 @@ def test_longest_paths_bitexact(gpu, orc, monkeypatch, group):
         assert np.array_equal(g["N"], o["N"])
 
 
-@pytest.mark.parametrize("method,n,cf", [(2, 5, 0.3), (1, 3, 0.3), (4, 3, 0.0)])
-def test_chains_equal_single_runs(gpu, method, n, cf):
+@pytest.mark.parametrize("launch", ["one", "streams"])
+@pytest.mark.parametrize("method,n,cf", [(2, 5, 0.3), (2, 10, 0.0), (1, 3, 0.3), (4, 3, 0.0)])
+def test_chains_equal_single_runs(gpu, method, n, cf, launch, monkeypatch):
     """pht_gibbs_run_chains (independent chains on their own contexts,
     streams and host threads): chain c is bit-identical to
-    the single chain run after set_seed(seeds[c])."""
+    the single chain run after set_seed(seeds[c]).  launch "one": the ECS
+    chains' exact ranges go out as one ecs_chains_kernel launch per sweep
+    (the default); "streams": one launch per chain on its own stream."""
+    if launch == "streams":
+        monkeypatch.setenv("PHT_CHAINS_LAUNCH", "streams")
+    else:
+        monkeypatch.delenv("PHT_CHAINS_LAUNCH", raising=False)
     S, s = bd_exit(n)
     y, cen = simulate_ph(S, s, 3000, seed=77 + n, censor_frac=cf)
     T, theta = bd_exit_structure(n)
@@ -211,3 +218,52 @@ def test_chains_equal_single_runs(gpu, method, n, cf):
         want = sw.gibbs(6, method, nu, zeta, T, Cm, zexp)
         assert np.array_equal(got[c], want), c
     assert not np.array_equal(got[0], got[1])
+
+
+def _run_chains_raw(ctx_list, seeds, it, method, nu, zeta, T, Cm, zexp):
+    import ctypes as C
+
+    L = P.load()
+    K, m = len(seeds), len(nu)
+    ctxs = (C.c_void_p * K)(*ctx_list)
+    res = np.zeros(K * it * m, np.float64)
+    Tf = np.ascontiguousarray(np.asarray(T).reshape(-1, order="F"), np.int32)
+    Cf = np.ascontiguousarray(np.asarray(Cm, np.float64).reshape(-1, order="F"))
+    kms = C.c_double(0.0)
+    rc = L.pht_gibbs_run_chains(ctxs, K, np.ascontiguousarray(seeds, np.uint32), it, method, m,
+                                np.ascontiguousarray(nu, np.float64), np.ascontiguousarray(zeta, np.float64),
+                                Tf, Cf, zexp, np.array([-1.0]), res, C.byref(kms))
+    assert rc == 0, L.pht_last_error().decode()
+    return res.reshape(K, m, it).transpose(0, 2, 1)
+
+
+def test_chains_one_launch_ragged(gpu, monkeypatch):
+    """One launch over 12 ECS chains with different data (sizes 0 .. 20000,
+    exact and censored mixes, one chain with no exact observation): each chain
+    is bit-identical to its single run.  12 chains exceed the hardware queues
+    a launch per stream could use at once."""
+    monkeypatch.delenv("PHT_CHAINS_LAUNCH", raising=False)
+    n, method, it = 5, 2, 5
+    S, s = bd_exit(n)
+    T, theta = bd_exit_structure(n)
+    nu, zeta = 1 + 50 * theta, np.full(len(theta), 50.0)
+    Cm = np.ones(T.shape)
+    sizes = [20000, 1, 0, 300, 7000, 64, 65, 4096, 2500, 12000, 3, 999]
+    cfs = [0.0, 0.0, 0.0, 0.3, 0.0, 1.0, 0.5, 0.0, 0.2, 0.0, 0.0, 0.1]
+    data = [simulate_ph(S, s, k, seed=500 + i, censor_frac=cf) for i, (k, cf) in enumerate(zip(sizes, cfs))]
+    zexp = P.zexp_for(np.concatenate([d[0] for d in data]))
+    seeds = [1000 + i for i in range(len(sizes))]
+    sws = []
+    try:
+        for y, cen in data:
+            sw = P.Sweeper(n, method, 1)
+            sw.set_obs(y, cen)
+            sws.append(sw)
+        got = _run_chains_raw([sw.ctx for sw in sws], seeds, it, method, nu, zeta, T, Cm, zexp)
+        for c, sw in enumerate(sws):
+            P.set_seed(seeds[c])
+            want = sw.gibbs(it, method, nu, zeta, T, Cm, zexp)
+            assert np.array_equal(got[c], want), (c, sizes[c])
+    finally:
+        for sw in sws:
+            sw.close()
