@@ -234,6 +234,19 @@ def main():
             except Exception as e:  # noqa: BLE001
                 log(f"[bench] cpu baseline failed: {e}")
                 line["cpu_baseline"] = None
+            # SURVEY.md §8(d)'s "best CPU" line: the reference on 16 host cores,
+            # observations split (a child process: this one has the GPU open)
+            try:
+                import subprocess
+
+                cmd = [sys.executable, "-m", "oracle.cpu_best", "--n", str(n), "--N", str(N), "--censor",
+                       str(args.censor), "--workers", "16", "--seconds", "10"]
+                out = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=180, check=True).stdout
+                line["cpu_best"] = json.loads(out.strip().splitlines()[-1])
+                line["cpu_best"]["ratio_gpu_over_cpu_best"] = line["value"] / line["cpu_best"]["value"]
+            except Exception as e:  # noqa: BLE001
+                log(f"[bench] cpu best line failed: {e}")
+                line["cpu_best"] = None
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
