@@ -356,6 +356,9 @@ struct pht_ctx {
   long dbg_cap = 0;
   float last_ms = 0.f;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  /* ECS: the censored range runs on stream2, concurrently with the exact range */
+  hipStream_t stream2 = nullptr;
+  hipEvent_t evf = nullptr, evj = nullptr;
   struct ChainGroup *grp = nullptr; /* pht_gibbs_run_chains: exact ECS launched with the other chains */
   int gidx = -1;
 };
@@ -574,7 +577,10 @@ extern "C" pht_ctx *pht_ctx_create(int device, int n, int method, int mhit) {
       hipMalloc(&c->d_stats, sizeof(unsigned long long) * stats_len(n)) != hipSuccess ||
       hipHostMalloc(&c->h_stats, sizeof(unsigned long long) * stats_len(n), 0) != hipSuccess ||
       hipHostMalloc(&c->h_params, make_layout(n).bytes(), 0) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evf, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evj, hipEventDisableTiming) != hipSuccess) {
     set_err("device %d: HIP allocation failed", device);
     delete c;
     return nullptr;
@@ -593,6 +599,9 @@ extern "C" void pht_ctx_destroy(pht_ctx *c) {
   if (c->h_params) (void)hipHostFree(c->h_params);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->evf) (void)hipEventDestroy(c->evf);
+  if (c->evj) (void)hipEventDestroy(c->evj);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -732,11 +741,25 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
      * tools/latency.py: -2 % kernel time at 1e6) */
     ae.newcap = getenv("PHT_NEWCAP") ? atoi(getenv("PHT_NEWCAP")) : 1;
     ae.spread = getenv("PHT_SPREAD") ? atoi(getenv("PHT_SPREAD")) : (c->n_exact <= 2 * kSpreadLanes);
-    if (ae.count > 0) HIPCHK(pht_launch_sweep(&ae, c->method, debug ? 1 : 0, c->stream));
     SweepArgs ac = a;
     ac.begin = c->n_exact;
     ac.count = c->count - c->n_exact;
-    if (ac.count > 0) HIPCHK(pht_launch_sweep(&ac, c->method, debug ? 1 : 0, c->stream));
+    /* both ranges: the censored kernel on stream2, concurrently, so each
+     * persistent kernel's tail (its longest paths) fills with the other's
+     * work; cfg5 ECS 2.49 -> 1.92 ms; the launch order does not matter
+     * (PHT_CENS_SERIAL=1: one stream) */
+    const bool fork = ae.count > 0 && ac.count > 0 && !getenv("PHT_CENS_SERIAL");
+    if (fork) {
+      HIPCHK(hipEventRecord(c->evf, c->stream));
+      HIPCHK(hipStreamWaitEvent(c->stream2, c->evf, 0));
+      HIPCHK(pht_launch_sweep(&ac, c->method, debug ? 1 : 0, c->stream2));
+      HIPCHK(hipEventRecord(c->evj, c->stream2));
+      HIPCHK(pht_launch_sweep(&ae, c->method, debug ? 1 : 0, c->stream));
+      HIPCHK(hipStreamWaitEvent(c->stream, c->evj, 0));
+    } else {
+      if (ae.count > 0) HIPCHK(pht_launch_sweep(&ae, c->method, debug ? 1 : 0, c->stream));
+      if (ac.count > 0) HIPCHK(pht_launch_sweep(&ac, c->method, debug ? 1 : 0, c->stream));
+    }
   } else {
     HIPCHK(pht_launch_sweep(&a, c->method, debug ? 1 : 0, c->stream));
   }
