@@ -185,6 +185,9 @@ def main():
                         "value = world x chain sweeps/s; `value` above is the BASELINE metric (strong, N fixed)"}
 
     if rank == 0:
+        # BASELINE.json's configurations by (n, N, censored fraction)
+        cfg_name = {(3, 200, 0.0): "cfg1", (5, 10_000, 0.0): "cfg2", (20, 100_000, 0.0): "cfg3",
+                    (10, 1_000_000, 0.0): "cfg4", (15, 500_000, 0.3): "cfg5"}.get((n, N, args.censor), "custom")
         sweeps_per_s = args.steps / dt
         local_obs = hi - lo
         achieved = ALG_BYTES_PER_OBS * local_obs / (kernel_ms * 1e-3) / 1e9
@@ -211,8 +214,8 @@ def main():
             "dtype": "f64",
             "data": f"synthetic: N={N} absorption times simulated from BD-exit(n={n}) (pi=e1), "
                     f"censored fraction {args.censor}, Philox key 0x{DATA_KEY:x}",
-            "config": {"workload": f"cfg4: phtMCMC2 {args.method}, n={n} states, m={m} parameters, "
-                                   f"N={N} exact obs, priors nu=1+50*theta, zeta=50, mhit=1",
+            "config": {"workload": f"{cfg_name}: phtMCMC2 {args.method}, n={n} states, m={m} parameters, "
+                                   f"N={N} obs ({args.censor:.0%} censored), priors nu=1+50*theta, zeta=50, mhit=1",
                        "n": n, "N": N, "method": args.method, "parallelism": f"obs-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
