@@ -4,6 +4,7 @@
  * sums for n in {3, 5, 10, 15, 20}, runtime-n loops otherwise).
  */
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "pht_kernels.h"
 #include "pht_layout.h"
@@ -24,6 +25,8 @@ extern "C" hipError_t pht_launch_sweep(const pht::SweepArgs *a, int method, int 
   using namespace pht;
   if (a->n < 1 || a->n > kMaxN) return hipErrorInvalidValue;
   if ((make_layout(a->n).bytes() & 15) != 0) return hipErrorInvalidValue;
+  static const bool generic = getenv("PHT_FORCE_NT0") != nullptr; /* A/B: runtime-n kernels only */
+  if (generic) return pht_launch_nt_0(a, method, debug, st);
   switch (a->n) {
     case 3: return pht_launch_nt_3(a, method, debug, st);
     case 5: return pht_launch_nt_5(a, method, debug, st);

@@ -1,0 +1,42 @@
+"""CPU: register budget of the hot kernels, read from the built library's
+gfx950 code objects (tools/kernel_regs.py; no GPU).
+
+The ECS kernels sit at the 256-VGPR edge of two waves per SIMD: a harmless
+looking source change once pushed ecs_exact_kernel<10> over it and cost 40 %
+at cfg4.  Bar: the single-chain and chains ECS kernels for
+n = 3, 5, 10 keep 2 waves per SIMD with no VGPR spills; the MHRS search keeps
+at least 4.
+"""
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+
+@pytest.fixture(scope="module")
+def regs(lib):
+    import kernel_regs
+    import phasetype_amd.build as B
+
+    return kernel_regs.kernels(B.LIB)
+
+
+@pytest.mark.parametrize("nt", [3, 5, 10])
+@pytest.mark.parametrize("kind", ["ecs_exact_kernelILi{nt}ELb0E", "ecs_chains_kernelILi{nt}EE"])
+def test_ecs_two_waves_no_spill(regs, nt, kind):
+    key = kind.format(nt=nt)
+    hits = {k: v for k, v in regs.items() if key in k}
+    assert len(hits) == 1, (key, list(hits))
+    (name, d), = hits.items()
+    assert d["waves_per_simd"] >= 2, (name, d)
+    assert d["vgpr_spill"] == 0, (name, d)
+
+
+def test_mhrs_search_occupancy(regs):
+    hits = {k: v for k, v in regs.items() if "mhrs_search" in k}
+    assert len(hits) >= 6 * 6  # 6 round widths x 6 compiled n
+    for name, d in hits.items():
+        assert d["waves_per_simd"] >= 4 and d["vgpr_spill"] == 0, (name, d)
