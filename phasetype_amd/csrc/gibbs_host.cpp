@@ -371,10 +371,11 @@ constexpr long kSpreadLanes = 256L * 2 * 256;
  * §8f.4).  Each chain's thread builds its parameters into its slot of one
  * pinned block and arrives; the last chain to arrive enqueues the whole sweep
  * of every arrived chain on the group's stream: one parameter upload, one
- * statistics reset, the censored-range kernels, ONE ecs_chains_kernel launch
- * over all exact ranges, one statistics download.  The others wait for that
- * sweep's `done` event.  A chain that stops (end of run or error) leaves the
- * group, so the others never wait for it.
+ * statistics reset, ONE ecs_chains_kernel launch over all exact ranges (the
+ * censored-range kernels concurrently on stream2), one statistics
+ * download.  The others wait for that sweep's `done` event.  A chain that
+ * stops (end of run or error) leaves the group, so the others never wait
+ * for it.
  */
 struct ChainGroup {
   int K = 0, device = 0, n = 0, pb = 0, sl = 0;
@@ -391,15 +392,20 @@ struct ChainGroup {
   SweepArgs *h_args = nullptr, *d_args = nullptr;           /* [K] packed */
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
   hipStream_t stream = nullptr;
+  /* censored ranges run on stream2, concurrently with the exact-range launch */
+  hipStream_t stream2 = nullptr;
+  hipEvent_t evf = nullptr, evj = nullptr;
 };
 
 static void group_destroy(ChainGroup *g) {
   if (!g) return;
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
-  for (hipEvent_t e : {g->ev0, g->ev1, g->done})
+  if (g->stream2) (void)hipStreamSynchronize(g->stream2);
+  for (hipEvent_t e : {g->ev0, g->ev1, g->done, g->evf, g->evj})
     if (e) (void)hipEventDestroy(e);
   if (g->stream) (void)hipStreamDestroy(g->stream);
+  if (g->stream2) (void)hipStreamDestroy(g->stream2);
   if (g->h_params) (void)hipHostFree(g->h_params);
   if (g->h_stats) (void)hipHostFree(g->h_stats);
   if (g->h_args) (void)hipHostFree(g->h_args);
@@ -424,6 +430,9 @@ static ChainGroup *group_create(int device, int K, int n) {
                   hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) == hipSuccess &&
                   hipEventCreate(&g->ev0) == hipSuccess && hipEventCreate(&g->ev1) == hipSuccess &&
                   hipEventCreateWithFlags(&g->done, hipEventDisableTiming) == hipSuccess &&
+                  hipStreamCreateWithFlags(&g->stream2, hipStreamNonBlocking) == hipSuccess &&
+                  hipEventCreateWithFlags(&g->evf, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&g->evj, hipEventDisableTiming) == hipSuccess &&
                   hipHostMalloc(&g->h_params, P, 0) == hipSuccess && hipMalloc(&g->d_params, P) == hipSuccess &&
                   hipHostMalloc(&g->h_stats, Sb, 0) == hipSuccess && hipMalloc(&g->d_stats, Sb) == hipSuccess &&
                   hipHostMalloc(&g->h_args, A, 0) == hipSuccess && hipMalloc(&g->d_args, A) == hipSuccess;
@@ -443,15 +452,25 @@ static void group_fire(ChainGroup *g) {
   if (e == hipSuccess)
     e = hipMemsetAsync(g->d_stats, 0, sizeof(unsigned long long) * g->sl * g->K, g->stream);
   if (e == hipSuccess) e = hipEventRecord(g->ev0, g->stream);
-  int nx = 0;
+  int nx = 0, nc = 0;
+  for (int i = 0; i < k; i++) {
+    const int w = g->who[i];
+    if (g->ex[w].count > 0) g->h_args[nx++] = g->ex[w];
+    if (g->ce[w].count > 0) nc++;
+  }
+  /* censored ranges on stream2 while the exact ranges run (as ctx_enqueue) */
+  const bool fork = nc > 0 && nx > 0;
+  if (e == hipSuccess && fork) e = hipEventRecord(g->evf, g->stream);
+  if (e == hipSuccess && fork) e = hipStreamWaitEvent(g->stream2, g->evf, 0);
   for (int i = 0; i < k && e == hipSuccess; i++) {
     const int w = g->who[i];
-    if (g->ce[w].count > 0) e = pht_launch_sweep(&g->ce[w], kMethodECS, 0, g->stream);
-    if (g->ex[w].count > 0) g->h_args[nx++] = g->ex[w];
+    if (g->ce[w].count > 0) e = pht_launch_sweep(&g->ce[w], kMethodECS, 0, fork ? g->stream2 : g->stream);
   }
+  if (e == hipSuccess && fork) e = hipEventRecord(g->evj, g->stream2);
   if (e == hipSuccess && nx > 0)
     e = hipMemcpyAsync(g->d_args, g->h_args, sizeof(SweepArgs) * nx, hipMemcpyHostToDevice, g->stream);
   if (e == hipSuccess && nx > 0) e = pht_launch_ecs_chains(g->h_args, g->d_args, nx, g->stream);
+  if (e == hipSuccess && fork) e = hipStreamWaitEvent(g->stream, g->evj, 0);
   if (e == hipSuccess) e = hipEventRecord(g->ev1, g->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(g->h_stats, g->d_stats, sizeof(unsigned long long) * g->sl * g->K, hipMemcpyDeviceToHost,
