@@ -402,8 +402,22 @@ __global__ void __launch_bounds__(kBlock) sweep_kernel(SweepArgs a) {
   sweep_body<NT, METHOD, DEBUG, EnvPrivate>(a);
 }
 
+/* waves per SIMD the persistent kernel is compiled for: the DCS kernel at
+ * n = 10 needs 410 VGPRs (one wave); held to two waves it spills 251 VGPRs
+ * outside its Brent loop and runs 11 % faster (cfg5-shaped n = 10: 3.09 ->
+ * 2.75 ms).  At n = 15 two waves are 19 % slower (5.65 -> 6.74 ms), so only
+ * n = 10 is held (tools/ab.py; PHT_PERSIST_WAVES=k forces every kernel). */
+#ifndef PHT_PERSIST_WAVES
+#define PHT_PERSIST_WAVES 0
+#endif
+template <int NT, int METHOD>
+constexpr int persist_waves() {
+  return PHT_PERSIST_WAVES > 0 ? PHT_PERSIST_WAVES : ((NT == 10 && METHOD == kMethodDCS) ? 2 : 1);
+}
 template <int NT, int METHOD, bool DEBUG>
-__global__ void __launch_bounds__(kBlock) persist_kernel(SweepArgs a) {
+__global__ void __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu(persist_waves<NT, METHOD>())))
+persist_kernel(SweepArgs a) {
   sweep_body<NT, METHOD, DEBUG, EnvPrivate, true>(a);
 }
 
