@@ -84,7 +84,9 @@ class RefLib:
         L.rshim_print_count.restype = C.c_long
         L.ref_gibbs.argtypes = [_ip, _ip, _ip, _ip, _ip, _dp, _dp, _ip, _dp, _dp, _ip, _ip, _dp, _ip, _dp]
         L.ref_eigen.argtypes = [C.c_int, _dp, _dp, _dp, _dp]
-        L.ref_sweep.argtypes = [C.c_int, C.c_int, _dp, _dp, C.c_int, _dp, _ip, C.c_int, C.c_int, _dp, _ip, _ip]
+        L.ref_sweep.argtypes = [C.c_int, C.c_int, _dp, _dp, C.c_int, _dp, _ip, C.c_int, C.c_int, _dp, _ip, _ip,
+                                _opt(_u32p)]
+        L.rshim_nword.restype = C.c_ulonglong
         L.rshim_get_state.argtypes = [np.ctypeslib.ndpointer(dtype=np.uint32), C.POINTER(C.c_int)]
 
     def set_seed(self, seed: int) -> None:
@@ -107,7 +109,9 @@ class RefLib:
         info = self.lib.ref_eigen(n, np.ascontiguousarray(S.reshape(-1, order="F")), ev, Q, Qi)
         return info, ev, Q.reshape(n, n, order="F"), Qi.reshape(n, n, order="F")
 
-    def sweep(self, method, S, s, y, censored=None, mhit=1, per_obs=True):
+    def sweep(self, method, S, s, y, censored=None, mhit=1, per_obs=True, nword=None):
+        """nword: optional uint32[l] array that receives the 32-bit MT words
+        each observation drew (per_obs only; the G4 fixtures)."""
         n = S.shape[0]
         y = np.ascontiguousarray(y, np.float64)
         l = len(y)
@@ -117,7 +121,7 @@ class RefLib:
         B = np.zeros(k if per_obs else n, np.int32)
         N = np.zeros(k * n * n, np.int32)
         self.lib.ref_sweep(method, n, np.ascontiguousarray(S.reshape(-1, order="F")), np.ascontiguousarray(s, np.float64),
-                           mhit, y, cen, l, int(per_obs), z, B, N)
+                           mhit, y, cen, l, int(per_obs), z, B, N, nword if per_obs else None)
         if per_obs:
             return B, z.reshape(l, n), N.reshape(l, n, n).transpose(0, 2, 1)  # N[obs, from, to]
         return B, z, N.reshape(n, n).T
@@ -167,7 +171,7 @@ class OracleLib:
         od, oi, ol, ou = _opt(_dp), _opt(_ip), _opt(_lp), _opt(_u32p)
         ostats = _opt(_lp)
         L.orc_ref_sweep.argtypes = [C.c_void_p, C.c_int, C.c_int, _dp, _ip, C.c_long, _dp, _ip, _ip,
-                                    oi, oi, od, oi, oi, ostats]
+                                    oi, oi, od, oi, oi, ou, ostats]
         L.orc_dev_sweep.argtypes = [C.c_void_p, C.c_int, C.c_int, _dp, _ip, C.c_long, C.c_long,
                                     C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, _lp, _lp, _lp,
                                     oi, oi, od, ol, oi, oi, ou, ostats]
@@ -194,14 +198,15 @@ class OracleLib:
         zt, Bt, Nt = np.zeros(n), np.zeros(n, np.int32), np.zeros(n * n, np.int32)
         if per_obs:
             B, pre, z = np.zeros(l, np.int32), np.zeros(l, np.int32), np.zeros(l * n)
-            N, fl = np.zeros(l * n * n, np.int32), np.zeros(l, np.int32)
+            N, fl, nw = np.zeros(l * n * n, np.int32), np.zeros(l, np.int32), np.zeros(l, np.uint32)
         else:
-            B = pre = z = N = fl = None
+            B = pre = z = N = fl = nw = None
         stats = np.zeros(4, np.int64)
-        self.lib.orc_ref_sweep(sp, method, mhit, y, cen, l, zt, Bt, Nt, B, pre, z, N, fl, stats)
+        self.lib.orc_ref_sweep(sp, method, mhit, y, cen, l, zt, Bt, Nt, B, pre, z, N, fl, nw, stats)
         out = dict(z_tot=zt, B_tot=Bt, N_tot=Nt.reshape(n, n).T, stats=stats)
         if per_obs:
-            out.update(B=B, pre=pre, z=z.reshape(l, n), N=N.reshape(l, n, n).transpose(0, 2, 1), flags=fl)
+            out.update(B=B, pre=pre, z=z.reshape(l, n), N=N.reshape(l, n, n).transpose(0, 2, 1), flags=fl,
+                       nword=nw)
         return out
 
     def dev_sweep(self, method, S, s, y, censored=None, mhit=1, key=(1, 2), sweep=1, zexp=None,

@@ -194,7 +194,7 @@ static int dispatch(int method) {
  */
 void orc_ref_sweep(const orc_sp *sp, int method, int mhit, const double *y, const int *cens, long l,
                    double *z_tot, int *B_tot, int *N_tot, int *B, int *pre, double *z, int *N, int *flags,
-                   long *stats) {
+                   uint32_t *nword, long *stats) {
   const int n = sp->n;
   int m = dispatch(method);
   orc_obs o;
@@ -202,6 +202,7 @@ void orc_ref_sweep(const orc_sp *sp, int method, int mhit, const double *y, cons
   for (int k = 0; k < n; k++) { z_tot[k] = 0.0; B_tot[k] = 0; }
   for (int k = 0; k < n * n; k++) N_tot[k] = 0;
   for (long i = 0; i < l; i++) {
+    const uint64_t w0 = g_rs.nword;
     if (m == ORC_MHRS) orcR_obs_mhrs(sp, y[i], cens[i], mhit, &g_rs, &o, 0.0);
     else if (m == ORC_DCS) orcR_obs_dcs(sp, y[i], &g_rs, &o, 0.0, &nbrent);
     else if (cens[i]) orcR_obs_censored(sp, y[i], cens[i], &g_rs, &o, 0.0, &neval);
@@ -210,6 +211,7 @@ void orc_ref_sweep(const orc_sp *sp, int method, int mhit, const double *y, cons
     for (int k = 0; k < n; k++) z_tot[k] += o.z[k];
     for (int k = 0; k < n * n; k++) N_tot[k] += o.N[k];
     put_obs(&o, n, i, B, pre, z, NULL, N, flags, NULL);
+    if (nword) nword[i] = (uint32_t)(g_rs.nword - w0); /* G4: MT words per observation */
   }
   if (stats) { stats[0] += neval; stats[1] += nbrent; }
 }
@@ -336,7 +338,7 @@ void orc_gibbs(int dev, int it, int mhit, int method, int n, int m, const double
     if (!disp) continue; /* "CRITICAL ERROR: Unknown sampling method" */
     orc_sp_build(sp, n, S, s, disp == ORC_MHRS ? ORC_MHRS : method);
     if (!dev) {
-      orc_ref_sweep(sp, method, mhit, y, censored, l, z, Bt, Nt, NULL, NULL, NULL, NULL, NULL, NULL);
+      orc_ref_sweep(sp, method, mhit, y, censored, l, z, Bt, Nt, NULL, NULL, NULL, NULL, NULL, NULL, NULL);
     } else {
       orc_dev_sweep(sp, method, mhit, y, censored, l, 0, k0, k1, (uint32_t)iter, zexp, zq, Bq, Nq, NULL, NULL,
                     NULL, NULL, NULL, NULL, NULL, NULL);

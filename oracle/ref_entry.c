@@ -65,14 +65,16 @@ int ref_eigen(int n, const double *S, double *evals, double *Q, double *Qinv) {
 /*
  * One step-1 sweep for fixed (S, s), method bitmask as LJMA_Gibbs.
  * per_obs != 0: outputs are per observation — z[l*n], B[l] (start state),
- * N[l*n*n] — by calling the sampler once per observation (the samplers keep
+ * N[l*n*n], nd[l] (32-bit MT words drawn; may be NULL) — by calling the
+ * sampler once per observation (the samplers keep
  * no state across observations other than the RNG stream, so the draws are
  * identical to one call over all observations).  per_obs == 0: z[n], B[n],
  * N[n*n] are the sampler's own accumulated totals.
  */
+unsigned long long rshim_nword(void);
 int ref_sweep(int method, int n, const double *S, const double *s, int mhit,
               const double *y, const int *censored, int l, int per_obs,
-              double *z, int *B, int *N) {
+              double *z, int *B, int *N, unsigned *nd) {
   double *P = (double *)calloc((size_t)n * n, sizeof(double));
   double *Pfull = (double *)calloc((size_t)n * (n + 1), sizeof(double));
   double *Q = (double *)calloc((size_t)n * n, sizeof(double));
@@ -132,12 +134,14 @@ int ref_sweep(int method, int n, const double *S, const double *s, int mhit,
     int mm = per_obs ? 1 : l;
     double *yp = (double *)y + (per_obs ? c : 0);
     int *cp = (int *)censored + (per_obs ? c : 0);
+    const unsigned long long w0 = rshim_nword();
     if (method & 0x1)
       LJMA_MHsample_Bladt(yp, cp, &mm, pi, Sc, sc, Pfull, &nn, &mh, rz, rB, rN, workD, workI);
     else if (method & 0x4)
       LJMA_MHsample_Hobolth2(yp, cp, &mm, pi, Sc, sc, Q, evals, Qinv_b, b, Qinv, &nn, &mh, rz, rB, rN, workD, workI);
     else if (method & 0x2)
       LJMA_MHsample_Aslett2(yp, cp, &mm, pi, Sc, sc, Q, evals, Qinv_s, Qinv_1, P, Pfull, &nn, rz, rB, rN, workD, workI);
+    if (per_obs && nd) nd[c] = (unsigned)(rshim_nword() - w0); /* G4: MT words per observation */
     if (per_obs) {
       int bs = 0;
       for (int k = 0; k < n; k++) if (rB[k]) bs = k;

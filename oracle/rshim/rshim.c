@@ -70,6 +70,8 @@ void rshim_free(void *p) { free(p); }
 /* ------------------------------------------------------------------ RNG */
 static pht_rstream g_rs;
 void rshim_set_seed(uint32_t seed) { pht_rs_set_seed(&g_rs, seed); }
+/* 32-bit MT words the reference has consumed since set_seed (G4 fixtures) */
+unsigned long long rshim_nword(void) { return (unsigned long long)g_rs.nword; }
 void rshim_get_state(uint32_t *mt624, int *mti) {
   memcpy(mt624, g_rs.mt, sizeof(g_rs.mt));
   *mti = g_rs.mti;

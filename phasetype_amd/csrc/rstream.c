@@ -27,6 +27,7 @@ void pht_rs_set_seed(pht_rstream *rs, uint32_t seed) {
     rs->mt[j] = seed;
   }
   rs->mti = MT_N;
+  rs->nword = 0;
 }
 
 static double mt_genrand(pht_rstream *rs) {
@@ -48,6 +49,7 @@ static double mt_genrand(pht_rstream *rs) {
     rs->mti = 0;
   }
   y = mt[rs->mti++];
+  rs->nword++;
   y ^= (y >> 11);
   y ^= (y << 7) & 0x9d2c5680U;
   y ^= (y << 15) & 0xefc60000U;

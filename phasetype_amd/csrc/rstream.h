@@ -32,6 +32,7 @@ extern "C" {
 typedef struct pht_rstream {
   uint32_t mt[624];
   int mti;
+  uint64_t nword; /* 32-bit MT outputs consumed since set_seed (draw-order checks) */
 } pht_rstream;
 
 void   pht_rs_set_seed(pht_rstream *rs, uint32_t seed);      /* set.seed(seed) */

@@ -58,6 +58,8 @@ def test_g3_per_observation_restatement(orc, n, method, mhit):
     assert np.array_equal(o["B"], d[k + "_B"])
     assert np.array_equal(o["z"], d[k + "_z"])
     assert np.array_equal(o["N"], d[k + "_N"].astype(np.int32))
+    # G4: the RNG consumption of every observation (MT words drawn)
+    assert np.array_equal(o["nword"], d[k + "_nw"])
 
 
 @pytest.mark.parametrize("n,method,mhit", G3[:4] + G3[8:])
@@ -65,9 +67,11 @@ def test_g3_reference_reproduces_fixture(ref, n, method, mhit):
     d = _load("g3_sweeps")
     k = f"n{n}_m{method}_h{mhit}"
     ref.set_seed(int(d[k + "_seed"]))
-    B, z, N = ref.sweep(method, d[f"n{n}_S"], d[f"n{n}_s"], d[f"n{n}_y"], d[f"n{n}_cen"], mhit=mhit)
+    nw = np.zeros(len(d[f"n{n}_y"]), np.uint32)
+    B, z, N = ref.sweep(method, d[f"n{n}_S"], d[f"n{n}_s"], d[f"n{n}_y"], d[f"n{n}_cen"], mhit=mhit, nword=nw)
     assert np.array_equal(B, d[k + "_B"]) and np.array_equal(z, d[k + "_z"])
     assert np.array_equal(N, d[k + "_N"].astype(np.int32))
+    assert np.array_equal(nw, d[k + "_nw"])
 
 
 def test_g1_reference_reproduces_fixture(ref):

@@ -14,6 +14,12 @@ GPU box), per SURVEY.md §8(c) G1–G3:
 * G3 ``g3_sweeps.npz`` — one step-1 sweep, per observation (start state B,
   z, N), for n in {3, 4, 10}, 100 exact + 100 censored observations, methods
   MHRS (mhit 1 and 5), ECS, DCS, one R stream per case.
+* G4 (keys ``*_nw`` of ``g3_sweeps.npz``) — the RNG consumption of each of
+  those observations: 32-bit Mersenne-Twister words the reference drew
+  (the draw-order check of Appendix A).
+
+usage: python3 tools/make_golden.py [g1_test_scripts g2_cfg1 g3_sweeps]
+(no names: all fixtures)
 """
 import os
 import sys
@@ -115,13 +121,15 @@ def g3(ref):
     for i, (n, method, mhit) in enumerate(G3_CASES):
         seed = 9000 + i
         ref.set_seed(seed)
+        nw = np.zeros(len(out[f"n{n}_y"]), np.uint32)
         B, z, N = ref.sweep(method, out[f"n{n}_S"], out[f"n{n}_s"], out[f"n{n}_y"], out[f"n{n}_cen"], mhit=mhit,
-                            per_obs=True)
+                            per_obs=True, nword=nw)
         k = f"n{n}_m{method}_h{mhit}"
         out[k + "_seed"] = np.int64(seed)
         out[k + "_B"] = B.astype(np.int32)
         out[k + "_z"] = z
         out[k + "_N"] = N.astype(np.int16)
+        out[k + "_nw"] = nw
     return out
 
 
@@ -130,7 +138,10 @@ def main():
         O.build(ref=True)
     ref = O.RefLib()
     os.makedirs(OUT, exist_ok=True)
+    want = set(sys.argv[1:])
     for name, fn in (("g1_test_scripts", g1), ("g2_cfg1", g2), ("g3_sweeps", g3)):
+        if want and name not in want:
+            continue
         d = fn(ref)
         np.savez_compressed(os.path.join(OUT, name + ".npz"), **d)
         print(name, os.path.getsize(os.path.join(OUT, name + ".npz")), "bytes")
