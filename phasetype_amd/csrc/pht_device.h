@@ -1075,20 +1075,26 @@ __device__ __forceinline__ void dcs(const Par<NT> &P, double y, Lane &ln, Sink &
   for (int i = 0; i < n; i++) a[i] = P.piQ(i) * pht_exp_neg(P.evals(i) * y);
   int b;
   {
-    double pend[PHT_VEC(NT)], sum = 0.0;
-#pragma unroll
+    /* end-state weights pend_k = (a Qinv)_k s_k, recomputed in the scan
+     * instead of kept in registers (same operations, so the same values):
+     * the kernel's register peak is here, outside the jump loop */
+    double sum = 0.0;
+#pragma unroll 1
     for (int k = 0; k < n; k++) {
       double acc = 0.0;
 #pragma unroll
       for (int i = 0; i < n; i++) acc = fma(a[i], P.Qinv(i, k), acc);
-      pend[k] = acc * P.s(k);
-      sum += pend[k];
+      sum += acc * P.s(k);
     }
     const double tg = dev_u(ln.r) * sum;
     double sofar = 0.0;
     int q = 0;
+#pragma unroll 1
     for (; q < n; q++) {
-      sofar += pend[q];
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) acc = fma(a[i], P.Qinv(i, q), acc);
+      sofar += acc * P.s(q);
       if (!(sofar < tg)) break;
     }
     if (q == n) {
