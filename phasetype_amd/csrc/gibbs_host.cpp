@@ -791,6 +791,13 @@ static int ctx_wait(pht_ctx *c) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  if (c->method == kMethodMHRS && c->d_mcnt && getenv("PHT_MHRS_COUNTS")) {
+    /* diagnostics: tasks still unresolved after MHRS search rounds 0..4 */
+    unsigned q[5];
+    HIPCHK(hipMemcpy(q, c->d_mcnt, sizeof q, hipMemcpyDeviceToHost));
+    fprintf(stderr, "[pht] MHRS unresolved after rounds 0-4: %u %u %u %u %u (of %ld tasks)\n", q[0], q[1], q[2],
+            q[3], q[4], c->count * (1 + c->mhit));
+  }
   return 0;
 }
 
