@@ -349,6 +349,7 @@ struct pht_ctx {
   unsigned long long *h_stats = nullptr; /* pinned */
   unsigned char *h_params = nullptr;     /* pinned */
   std::vector<long> order;               /* sorted position -> local index */
+  std::vector<double> h_ysorted;         /* y in device (sorted) order */
   /* debug buffers */
   long long *d_zq = nullptr;
   int *d_N = nullptr, *d_B = nullptr, *d_pre = nullptr, *d_flags = nullptr;
@@ -661,6 +662,7 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
   }
   c->n_exact = 0;
   while (c->n_exact < count && cs[c->n_exact] == 0) c->n_exact++;
+  c->h_ysorted = ys;
   c->order = std::move(ord);
   HIPCHK(hipMalloc(&c->d_y, sizeof(double) * count));
   HIPCHK(hipMalloc(&c->d_cens, sizeof(int) * count));
@@ -760,6 +762,11 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
      * tools/latency.py: -2 % kernel time at 1e6) */
     ae.newcap = getenv("PHT_NEWCAP") ? atoi(getenv("PHT_NEWCAP")) : 1;
     ae.spread = getenv("PHT_SPREAD") ? atoi(getenv("PHT_SPREAD")) : (c->n_exact <= 2 * kSpreadLanes);
+    /* PHT_HOT=k: the remaining-time threshold is the k-th longest exact y */
+    {
+      const long hk = getenv("PHT_HOT") ? atol(getenv("PHT_HOT")) : 0;
+      ae.hoty = (hk > 0 && hk <= c->n_exact) ? c->h_ysorted[hk - 1] : 0.0;
+    }
     SweepArgs ac = a;
     ac.begin = c->n_exact;
     ac.count = c->count - c->n_exact;

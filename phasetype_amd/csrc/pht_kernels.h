@@ -32,6 +32,7 @@ struct SweepArgs {
   int occ;                     /* ECS exact: blocks per CU of the persistent grid (0 = occupancy limit) */
   int spread;                  /* ECS exact: first claims lane-major (the longest paths one per wavefront) */
   int newcap;                  /* ECS exact: observations a lane may start per round (0 = no limit) */
+  double hoty;                 /* ECS exact: waves with a path whose remaining time exceeds hoty issue at high priority (0 = off) */
   /* MHRS attempt search (pht_kernels.hip, MHRS section): per chain task
    * (position * (1 + mhit) + c) its first success (attempt << 8 | pre), two
    * task queues and the queue counters; allocated by the host for MHRS */

@@ -645,6 +645,12 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
     }
     PHT_STAMP(ln, 0);
     if (!__any(need) && !__any(pend)) break;
+    /* the waves carrying the longest remaining paths issue first, so the
+     * sweep's critical path is not slowed by the others */
+    if (a.hoty > 0.0) {
+      if (__any(have && st.yt > a.hoty)) __builtin_amdgcn_s_setprio(3);
+      else __builtin_amdgcn_s_setprio(0);
+    }
 #ifdef PHT_STAMPS
     ln.st_rounds++;
 #endif

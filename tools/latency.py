@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Kernel time of the ECS-exact sweep against the shard size (strong-scaling
 regime) for the launch variants the host can pick at run time:
-PHT_GROUP (lanes per observation) and PHT_ECS_OCC (blocks per CU).
+PHT_GROUP (lanes per observation), PHT_ECS_OCC (blocks per CU), PHT_HOT
+(variant hotK: wave priority for the K longest remaining paths), base = defaults.
 
 usage (GPU box): python3 tools/latency.py [--Ns 62500 125000 ...] [--sweeps 8]
 Shard = the first N observations of the bench data set (what rank 0 of
@@ -56,7 +57,12 @@ def main():
             os.environ.pop("PHT_ECS_OCC", None)
             os.environ.pop("PHT_SPREAD", None)
             os.environ.pop("PHT_NEWCAP", None)
-            if v.startswith("nc"):
+            os.environ.pop("PHT_HOT", None)
+            if v == "base":
+                pass
+            elif v.startswith("hot"):  # waves with one of the K longest remaining paths at high priority
+                os.environ["PHT_HOT"] = v[3:]
+            elif v.startswith("nc"):
                 os.environ["PHT_GROUP"] = "1"
                 os.environ["PHT_NEWCAP"] = v[2:]
             elif v == "sp":
