@@ -164,6 +164,27 @@ def test_grid_occupancy_invariance(gpu, monkeypatch, occ):
     assert np.array_equal(ref[:2 * n + n * n], got[:2 * n + n * n])
 
 
+@pytest.mark.parametrize("knob,value", [("PHT_CENS_SERIAL", "1"), ("PHT_HOT", "500"), ("PHT_NEWCAP", "0"),
+                                        ("PHT_SPREAD", "1"), ("PHT_FORCE_NT0", "1")])
+def test_launch_knobs_invariance(gpu, monkeypatch, knob, value):
+    """Launch-shape knobs (serial censored range, wave priority, no new-
+    observation cap, lane-major first claims, runtime-n kernels) change no
+    statistic: 30 % censored ECS at n = 10.  PHT_FORCE_NT0 is read once per
+    process, so it is exercised only if no earlier launch cached it."""
+    n = 10
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 20000, seed=37, censor_frac=0.3)
+    zexp = P.zexp_for(y)
+    sw = P.Sweeper(n, 2)
+    sw.set_obs(y, cen)
+    ref = sw.sweep(S, s, key=(2, 8), sweep=3, zexp=zexp)
+    monkeypatch.setenv(knob, value)
+    got = sw.sweep(S, s, key=(2, 8), sweep=3, zexp=zexp)
+    sw.close()
+    L = 2 * n + n * n
+    assert np.array_equal(ref[:L], got[:L])
+
+
 @pytest.mark.parametrize("group", [1, 2, 4, 8])
 def test_longest_paths_bitexact(gpu, orc, monkeypatch, group):
     """The longest latent paths (the 4096 largest of 1e6 absorption times:
