@@ -548,11 +548,20 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
   double lastd;
   double Elast[PHT_VEC(NT)];
   double lammax;            /* max_i |lambda_i| (init4) */
-  double Wr[PHT_VEC(NT)];   /* W[j, .] in registers */
+  /* W[j, .] in registers, except at n >= 15, where it is read from the LDS
+   * parameter block (the registers go to a second wave instead) */
+  static constexpr bool kWrReg = !(NT >= 15);
+  double Wr[kWrReg ? PHT_VEC(NT) : 1];
+  __device__ __forceinline__ double w(int i) const {
+    if constexpr (kWrReg) return Wr[i];
+    else return P.W(j, i);
+  }
   __device__ __forceinline__ void load(double lam) {
     const int n = P.n();
+    if constexpr (kWrReg) {
 #pragma unroll
-    for (int i = 0; i < n; i++) Wr[i] = P.W(j, i);
+      for (int i = 0; i < n; i++) Wr[i] = P.W(j, i);
+    }
     lammax = lam;
   }
   __device__ __forceinline__ double operator()(double d) {
@@ -565,7 +574,7 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
 #pragma unroll
       for (int i = 0; i < n; i++) Elast[i] = pht_exp_neg(P.evals(i) * x);
     }
-    const double acc = dev_dot16([&](int i) { return Wr[i]; }, Elast, n);
+    const double acc = dev_dot16([&](int i) { return w(i); }, Elast, n);
     lastd = d;
     return pht_log(acc) + Sjj * d;
   }
@@ -574,7 +583,7 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
   static constexpr bool kInit4 = true;
   __device__ __forceinline__ void init4(const double xinit[4], double yv[4]) {
     const int n = P.n();
-    auto Wj = [&](int i) { return Wr[i]; };
+    auto Wj = [&](int i) { return w(i); };
     const double x3 = y_t - xinit[3];
     double acc[4];
     if (pht_ecs_init_ok(lammax, xinit[0], x3)) {

@@ -684,11 +684,16 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
     if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
 }
 
+/* waves per SIMD the ECS kernel is compiled for: two at n = 15, where the
+ * W row read from LDS (EcsDens) brings it to 258 VGPRs; otherwise what the
+ * registers allow (PHT_ECS_WAVES=k forces every n) */
+template <int NT>
+constexpr int ecs_waves() {
+  return PHT_ECS_WAVES > 0 ? PHT_ECS_WAVES : (NT == 15 ? 2 : 1);
+}
 template <int NT, bool DEBUG>
 __global__ void __launch_bounds__(kBlock)
-#if PHT_ECS_WAVES > 0
-__attribute__((amdgpu_waves_per_eu(PHT_ECS_WAVES, PHT_ECS_WAVES)))
-#endif
+__attribute__((amdgpu_waves_per_eu(ecs_waves<NT>())))
 ecs_exact_kernel(SweepArgs a) {
   ecs_exact_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
 }
@@ -702,9 +707,7 @@ ecs_exact_kernel(SweepArgs a) {
  */
 template <int NT>
 __global__ void __launch_bounds__(kBlock)
-#if PHT_ECS_WAVES > 0
-__attribute__((amdgpu_waves_per_eu(PHT_ECS_WAVES, PHT_ECS_WAVES)))
-#endif
+__attribute__((amdgpu_waves_per_eu(ecs_waves<NT>())))
 ecs_chains_kernel(const SweepArgs *args, int K, unsigned nblk) {
   const SweepArgs a = args[blockIdx.x % (unsigned)K];
   ecs_exact_body<NT, false>(a, blockIdx.x / (unsigned)K, nblk);
