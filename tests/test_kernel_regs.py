@@ -4,8 +4,8 @@ gfx950 code objects (tools/kernel_regs.py; no GPU).
 The ECS kernels sit at the 256-VGPR edge of two waves per SIMD: a harmless
 looking source change once pushed ecs_exact_kernel<10> over it and cost 40 %
 at cfg4.  Bar: the single-chain and chains ECS kernels for
-n = 3, 5, 10 keep 2 waves per SIMD with no VGPR spills; the MHRS search keeps
-at least 4.
+n = 3, 5, 10, 15 keep 2 waves per SIMD with no VGPR spills; the MHRS search
+keeps at least 4.
 """
 import os
 import sys
@@ -24,7 +24,7 @@ def regs(lib):
     return kernel_regs.kernels(B.LIB)
 
 
-@pytest.mark.parametrize("nt", [3, 5, 10])
+@pytest.mark.parametrize("nt", [3, 5, 10, 15])
 @pytest.mark.parametrize("kind", ["ecs_exact_kernelILi{nt}ELb0E", "ecs_chains_kernelILi{nt}EE"])
 def test_ecs_two_waves_no_spill(regs, nt, kind):
     key = kind.format(nt=nt)
