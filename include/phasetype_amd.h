@@ -66,6 +66,12 @@ int pht_ctx_sweep_debug(pht_ctx *c, const double *S, const double *s, uint32_t k
                         int zexp, long long *stats_out, int *B, int *pre, int *flags, uint32_t *ndraw,
                         long long *zq, int *N);
 float pht_ctx_last_kernel_ms(pht_ctx *c);
+/* Observation-sweeps flagged in the last pht_gibbs_run / pht_gibbs_run_chains
+ * on this context (node-wide, after the reduce): a cap (ARMS iterations, path
+ * length, MHRS attempts) or a numerical guard fired, and the observation
+ * contributed its last attempt.  No reference counterpart (its loops are
+ * unbounded); a warning is also printed once per run. */
+long long pht_ctx_flagged_obs(pht_ctx *c);
 
 /* Gibbs loop over one shard; reduce(stats, len, user) must sum the int64
  * block across all shards (return 0 on success). */
@@ -79,7 +85,10 @@ int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double *nu, const
  * chain c on ctxs[c] (one context each, same n/method/mhit, observations set),
  * its own host thread and R-compatible stream seeded by seeds[c]; chain c
  * equals pht_gibbs_run after pht_set_seed(seeds[c]).  res: nchains blocks of
- * it*m (pht_gibbs_run's layout); start: nchains*m values or start[0] < 0.
+ * it*m (pht_gibbs_run's layout); start: exactly nchains*m values (chain c
+ * reads start[c*m .. c*m+m-1]) or start[0] < 0 — the length is not checked
+ * here, so a caller holding one m-vector must repeat it per chain (the
+ * Python mirror phasetype_amd.gibbs_chains broadcasts and validates it).
  * Standalone builds only (fails inside R). */
 int pht_gibbs_run_chains(pht_ctx **ctxs, int nchains, const uint32_t *seeds, int it, int method, int m,
                          const double *nu, const double *zeta, const int *T, const double *C, int zexp,

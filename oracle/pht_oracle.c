@@ -249,12 +249,16 @@ void orc_dev_sweep(const orc_sp *sp, int method, int mhit, const double *y, cons
   if (stats) { stats[0] += neval; stats[1] += nbrent; }
 }
 
-/* fixed-point exponent for z: 52 - ceil(log2(sum(y) + 1)) */
+/* fixed-point exponent for z: 52 - e with sum(y) < 2^e;
+ * 52 for an empty, zero or non-finite sum; clamped to [-1000, 1000] */
 int orc_zexp(const double *y, long l) {
   double sy = 0.0;
   for (long i = 0; i < l; i++) sy += y[i];
-  int e = (int)ceil(log2(sy + 1.0));
-  return 52 - e;
+  if (!(sy > 0.0) || !isfinite(sy)) return 52;
+  int e = 0;
+  (void)frexp(sy, &e);
+  int z = 52 - e;
+  return z > 1000 ? 1000 : (z < -1000 ? -1000 : z);
 }
 
 /* ---------------------------------------------------------- Gibbs driver */

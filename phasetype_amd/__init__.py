@@ -46,7 +46,8 @@ EXPORTS = [
     "LJMA_Gibbs", "R_init_PhaseType", "pht_last_error", "pht_device_count", "pht_bind_lapack", "pht_set_seed",
     "pht_unif_rand", "pht_rgamma", "pht_in_R", "pht_set_verbose", "pht_zexp", "pht_params_bytes", "pht_stats_len",
     "pht_build_params", "pht_ctx_create", "pht_ctx_destroy", "pht_ctx_set_obs", "pht_ctx_sweep",
-    "pht_ctx_sweep_debug", "pht_ctx_last_kernel_ms", "pht_gibbs_run", "pht_gibbs_run_chains",
+    "pht_ctx_sweep_debug", "pht_ctx_last_kernel_ms", "pht_ctx_flagged_obs", "pht_gibbs_run",
+    "pht_gibbs_run_chains",
 ]
 
 
@@ -93,6 +94,8 @@ def load(build_if_needed: bool = True) -> C.CDLL:
                                       _ip, _ip, _ip, _up, _lp, _ip]
     L.pht_ctx_last_kernel_ms.restype = C.c_float
     L.pht_ctx_last_kernel_ms.argtypes = [C.c_void_p]
+    L.pht_ctx_flagged_obs.restype = C.c_longlong
+    L.pht_ctx_flagged_obs.argtypes = [C.c_void_p]
     L.pht_gibbs_run.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _dp, C.c_int, C.c_int,
                                 _dp, _dp, C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]
     L.pht_gibbs_run_chains.argtypes = [C.POINTER(C.c_void_p), C.c_int, _up, C.c_int, C.c_int, C.c_int, _dp, _dp,
@@ -146,6 +149,7 @@ class Sweeper:
         if not self.ctx:
             raise _err(self.L)
         self.count = 0
+        self.flagged_obs = 0  # flagged observation-sweeps of the last gibbs() (pht_ctx_flagged_obs)
 
     def set_obs(self, y, censored=None, obs0: int = 0):
         y = np.ascontiguousarray(y, np.float64)
@@ -204,6 +208,7 @@ class Sweeper:
         if rc != 0:
             raise _err(self.L)
         self.kernel_ms_total = kms.value
+        self.flagged_obs = int(self.L.pht_ctx_flagged_obs(self.ctx))
         return res.reshape(m, it).T.copy()
 
     def close(self):
@@ -216,6 +221,24 @@ class Sweeper:
             self.close()
         except Exception:  # noqa: BLE001
             pass
+
+
+def _chains_start(start, K: int, m: int) -> np.ndarray:
+    """The start block pht_gibbs_run_chains reads: [-1] (draw from the prior),
+    or K*m values, chain c at [c*m, (c+1)*m).  A single m-vector (what
+    Sweeper.gibbs and the R API take) is broadcast to every chain; any other
+    length is refused here, because the C side reads start + c*m unchecked."""
+    if start is None:
+        return np.array([-1.0])
+    st = np.ascontiguousarray(start, np.float64).reshape(-1)
+    if st.size >= 1 and st[0] < 0:
+        return np.array([-1.0])
+    if st.size == m:
+        return np.ascontiguousarray(np.tile(st, K))
+    if st.size == K * m:
+        return st
+    raise ValueError(f"gibbs_chains: start has {st.size} values; need {m} (one start for every chain) "
+                     f"or {K}*{m} (one per chain), or a negative first value")
 
 
 def gibbs_chains(seeds, y, censored, n, method, nu, zeta, T, C_, mhit: int = 1, it: int = 100, start=None,
@@ -234,7 +257,7 @@ def gibbs_chains(seeds, y, censored, n, method, nu, zeta, T, C_, mhit: int = 1, 
             sws.append(sw)
         ctxs = (C.c_void_p * K)(*[sw.ctx for sw in sws])
         res = np.zeros(K * it * m, np.float64)
-        st = np.array([-1.0]) if start is None else np.ascontiguousarray(start, np.float64).reshape(-1)
+        st = _chains_start(start, K, m)
         Tf = np.ascontiguousarray(np.asarray(T).reshape(-1, order="F"), np.int32)
         Cf = np.ascontiguousarray(np.asarray(C_, np.float64).reshape(-1, order="F"))
         kms = C.c_double(0.0)

@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <condition_variable>
 #include <mutex>
 #include <numeric>
@@ -114,6 +115,22 @@ void say(const char *fmt, ...) {
   } else if (g_verbose) {
     fputs(buf, stdout);
     fflush(stdout);
+  }
+}
+/* a warning the caller must see: Rprintf inside R, stderr otherwise */
+void warn(const char *fmt, ...) {
+  RHost &h = rhost();
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (h.inR) {
+    h.rprintf("%s", buf);
+    if (h.flush) h.flush();
+  } else {
+    fputs(buf, stderr);
+    fflush(stderr);
   }
 }
 }  // namespace
@@ -362,6 +379,7 @@ struct pht_ctx {
   hipEvent_t evf = nullptr, evj = nullptr;
   struct ChainGroup *grp = nullptr; /* pht_gibbs_run_chains: exact ECS launched with the other chains */
   int gidx = -1;
+  long long flagged = 0; /* flagged observation-sweeps of the last Gibbs run (node-wide) */
 };
 
 /* lanes of the persistent ECS grid on an MI355X (256 CUs x 2 blocks x 256) */
@@ -854,12 +872,20 @@ extern "C" int pht_ctx_sweep_debug(pht_ctx *c, const double *S, const double *s,
 }
 
 extern "C" float pht_ctx_last_kernel_ms(pht_ctx *c) { return c->last_ms; }
+extern "C" long long pht_ctx_flagged_obs(pht_ctx *c) { return c->flagged; }
 
-/* fixed-point exponent for z (52 - ceil(log2(sum y + 1))) */
+/* fixed-point exponent for z: 52 - e with sum(y) < 2^e
+ * (frexp), so the exact-observation total stays below 2^52 whatever the
+ * time scale of the data (11 bits of int64 headroom are left for censored
+ * paths running past y).  Clamped so 2^zexp is a finite normal double;
+ * an empty, zero or non-finite sum gives 52. */
 extern "C" int pht_zexp(const double *y, long l) {
   double sy = 0.0;
   for (long i = 0; i < l; i++) sy += y[i];
-  return 52 - (int)ceil(log2(sy + 1.0));
+  if (!(sy > 0.0) || !std::isfinite(sy)) return 52;
+  int e = 0;
+  (void)frexp(sy, &e);
+  return std::min(1000, std::max(-1000, 52 - e));
 }
 
 /* ============================================================ Gibbs core */
@@ -965,6 +991,8 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
   say("Starting phase-type MCMC sampler ...\n\nBegining processing ...");
   if (silent) say(" silent processing selected, there will be no further feedback until MCMC run complete");
   double kms = 0.0;
+  long long flagged = 0;
+  int first_flagged = 0;
   for (int iter = 1; iter < it; iter++) {
     if (!silent) say("\rProcessing iteration %d of %d (%.1lf%%)\r", iter + 1, it, (100.0 * (iter + 1)) / it);
     if (!disp) {
@@ -991,9 +1019,22 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
       set_err("statistics all-reduce callback failed at sweep %d", iter);
       return -1;
     }
+    /* observations that hit a cap (ARMS iterations, path length, MHRS
+     * attempts) or a numerical guard contribute their last attempt, where
+     * the reference would keep looping (DESIGN.md §3 Caps) */
+    const long long fl = tot[2 * n + n * n + 2];
+    if (fl > 0) {
+      if (!first_flagged) first_flagged = iter;
+      flagged += fl;
+    }
     for (int k = 0; k < n; k++) z[k] = ldexp((double)tot[k], -zexp);
     G.update(R, iter, z.data(), tot.data() + 2 * n);
   }
+  for (pht_ctx *c : ctxs) c->flagged = flagged;
+  if (flagged)
+    warn("\nWARNING: %lld observation-sweeps hit a sampler cap or numerical guard (first in iteration %d); "
+         "each contributed its last attempt to the sufficient statistics\n",
+         flagged, first_flagged + 1);
   if (kernel_ms_total) *kernel_ms_total = kms;
   return 0;
 }

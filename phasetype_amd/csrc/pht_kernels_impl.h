@@ -430,34 +430,43 @@ static int smem_bytes(int n) {
 /*
  * Per-kernel launch configuration, shared by every host thread that
  * launches the kernel (pht_gibbs_run_chains runs chains from several
- * threads): the dynamic-LDS limit is raised whenever a larger footprint is
- * launched (the runtime-n kernels see several n per process) and the
- * occupancy is queried again after it; a mutex orders all of it.
+ * threads), kept per device: LJMA_Gibbs drives every visible GPU from one
+ * process, and both the dynamic-LDS limit (hipFuncSetAttribute) and the
+ * device properties are per device.  The limit is raised whenever a larger
+ * footprint is launched on that device (the runtime-n kernels see several n
+ * per process) and the occupancy is queried again after it; a mutex orders
+ * all of it.
  */
+constexpr int kMaxDevices = 64;
 struct LaunchCfg {
+  struct Dev {
+    int occ = -1, cus = 0, lds = 0, occ_sm = -1;
+  };
   std::mutex m;
-  int occ = -1, cus = 0, lds = 0, occ_sm = -1;
+  Dev d[kMaxDevices];
 };
 
 static hipError_t launch_config(LaunchCfg &cfg, const void *kernel, int sm, int *occ, int *cus) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> lock(cfg.m);
-  if (sm > cfg.lds) {
+  LaunchCfg::Dev &c = cfg.d[dev];
+  if (sm > c.lds) {
     if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, sm) != hipSuccess)
       return hipErrorUnknown;
-    cfg.lds = sm;
+    c.lds = sm;
   }
-  if (cfg.occ < 0 || sm != cfg.occ_sm) {
-    cfg.occ_sm = sm;
-    int dev = 0;
+  if (c.occ < 0 || sm != c.occ_sm) {
+    c.occ_sm = sm;
     hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return hipErrorUnknown;
     int b = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kBlock, sm) != hipSuccess || b < 1) b = 1;
-    cfg.cus = prop.multiProcessorCount;
-    cfg.occ = b;
+    c.cus = prop.multiProcessorCount;
+    c.occ = b;
   }
-  *occ = cfg.occ;
-  *cus = cfg.cus;
+  *occ = c.occ;
+  *cus = c.cus;
   return hipSuccess;
 }
 
@@ -685,8 +694,11 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
 }
 
 /* waves per SIMD the ECS kernel is compiled for: two at n = 15, where the
- * W row read from LDS (EcsDens) brings it to 258 VGPRs; otherwise what the
- * registers allow (PHT_ECS_WAVES=k forces every n) */
+ * W row read from LDS (EcsDens) lets it fit (255 VGPRs, no spills, per the
+ * built library's metadata: tools/kernel_regs.py); otherwise what the
+ * registers allow (PHT_ECS_WAVES=k forces every n).  The DEBUG=true
+ * instantiations (per-observation outputs for the parity tests) may spill a
+ * few VGPRs: they are never timed. */
 template <int NT>
 constexpr int ecs_waves() {
   return PHT_ECS_WAVES > 0 ? PHT_ECS_WAVES : (NT == 15 ? 2 : 1);

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import phasetype_amd as P
-from phasetype_amd.synth import bd_exit, simulate_ph
+from phasetype_amd.synth import bd_exit, bd_exit_structure, simulate_ph
 
 pytestmark = pytest.mark.gpu
 
@@ -59,6 +59,33 @@ def test_zero_and_tiny_times(gpu, orc, method):
     _check(orc, 4, method, y, cen)
 
 
+@pytest.mark.parametrize("method", [1, 2, 4])
+@pytest.mark.parametrize("scale", [1e-10, 1e3])
+def test_time_scale(gpu, orc, method, scale):
+    """Data on a sub-nanosecond (or a long) time scale: rates S/scale,
+    times y*scale.  Per observation identical to the oracle, and the
+    fixed-point z of each exact observation sums back to its y within
+    1e-12 relative (pht_zexp follows sum(y), so the quantum scales with
+    the data: ADVICE r01)."""
+    n = 4
+    S0, s0 = bd_exit(n)
+    S, s = S0 / scale, s0 / scale
+    y, cen = simulate_ph(S0, s0, 300, seed=31, censor_frac=0.3)
+    y = np.ascontiguousarray(y * scale)
+    zexp = int(orc.lib.orc_zexp(y, len(y)))
+    assert zexp == P.zexp_for(y)
+    sw = P.Sweeper(n, method, 1)
+    sw.set_obs(y, cen)
+    g = sw.sweep_debug(S, s, key=(9, 4), sweep=3, zexp=zexp)
+    sw.close()
+    o = orc.dev_sweep(method, S, s, y, cen, mhit=1, key=(9, 4), sweep=3, zexp=zexp)
+    for f in FIELDS:
+        assert np.array_equal(g[f], o[f]), f
+    ok = (cen == 0) & (g["flags"] == 0) & (y > 0)
+    tot = np.ldexp(g["zq"].sum(axis=1).astype(np.float64), -zexp)
+    assert np.all(np.abs(tot[ok] - y[ok]) <= 1e-12 * y[ok])
+
+
 @pytest.mark.parametrize("method", [1, 2])
 def test_all_censored(gpu, orc, method):
     S, s = bd_exit(6)
@@ -79,6 +106,33 @@ def test_mhrs_single_hard_observation(gpu, orc):
     S, s = bd_exit(3)
     y = np.array([9.0])
     _check(orc, 3, 1, y, np.zeros(1, np.int32), mhit=2)
+
+
+def test_flagged_observations_reported(gpu, capfd):
+    """An exact observation no MHRS attempt can reach (survival ~e^-60) hits
+    the 2^22-attempt cap in every sweep: the Gibbs run counts it
+    (Sweeper.flagged_obs, pht_ctx_flagged_obs) and warns once (ADVICE r01);
+    clean data reports none and prints nothing."""
+    n = 3
+    S, s = bd_exit(n)
+    T, theta = bd_exit_structure(n)
+    nu, zeta, Cm = 1 + 50 * theta, np.full(len(theta), 50.0), np.ones(T.shape)
+    y, cen = simulate_ph(S, s, 300, seed=4)
+    sw = P.Sweeper(n, 1, 1)
+    sw.set_obs(y, cen)
+    P.set_seed(2)
+    sw.gibbs(3, 1, nu, zeta, T, Cm, P.zexp_for(y))
+    assert sw.flagged_obs == 0
+    assert "WARNING" not in capfd.readouterr().err
+    y2 = y.copy()
+    y2[7] = 300.0
+    sw.set_obs(y2, cen)
+    P.set_seed(2)
+    sw.gibbs(3, 1, nu, zeta, T, Cm, P.zexp_for(y2))
+    sw.close()
+    assert sw.flagged_obs == 2  # one observation in each of the 2 sampled sweeps
+    err = capfd.readouterr().err
+    assert err.count("WARNING") == 1 and "2 observation-sweeps" in err
 
 
 @pytest.mark.parametrize("n", [1, 2, 3])

@@ -241,6 +241,32 @@ def test_chains_equal_single_runs(gpu, method, n, cf, launch, monkeypatch):
     assert not np.array_equal(got[0], got[1])
 
 
+@pytest.mark.parametrize("per_chain", [False, True])
+def test_chains_with_start(gpu, per_chain):
+    """A user start: one m-vector is broadcast to every chain, or K*m values
+    give each chain its own; chain c equals Sweeper.gibbs from that start."""
+    n, method = 5, 2
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 2000, seed=5, censor_frac=0.2)
+    T, theta = bd_exit_structure(n)
+    m = len(theta)
+    nu, zeta = 1 + 50 * theta, np.full(m, 50.0)
+    Cm = np.ones(T.shape)
+    seeds = [3, 4, 5]
+    starts = np.stack([theta * (1.0 + 0.1 * c) for c in range(len(seeds))])
+    arg = starts.reshape(-1) if per_chain else starts[0]
+    got, _ = P.gibbs_chains(seeds, y, cen, n, method, nu, zeta, T, Cm, it=5, start=arg)
+    zexp = P.zexp_for(y)
+    sw = P.Sweeper(n, method, 1)
+    sw.set_obs(y, cen)
+    for c, sd in enumerate(seeds):
+        P.set_seed(sd)
+        st = starts[c] if per_chain else starts[0]
+        want = sw.gibbs(5, method, nu, zeta, T, Cm, zexp, start=st)
+        assert np.array_equal(got[c], want), c
+        assert np.array_equal(got[c][0], st)
+
+
 def _run_chains_raw(ctx_list, seeds, it, method, nu, zeta, T, Cm, zexp):
     import ctypes as C
 

@@ -72,6 +72,23 @@ def test_no_cpu_fallback_ljma_gibbs():
                      np.zeros(9))
 
 
+def test_chains_start_block():
+    """gibbs_chains' start: one m-vector broadcast to all K chains, K*m
+    values kept, prior draw kept as [-1]; other lengths refused (the C side
+    reads start + c*m without a length)."""
+    K, m = 3, 4
+    assert np.array_equal(P._chains_start(None, K, m), [-1.0])
+    assert np.array_equal(P._chains_start([-1.0], K, m), [-1.0])
+    one = np.arange(1.0, m + 1)
+    assert np.array_equal(P._chains_start(one, K, m), np.tile(one, K))
+    per = np.arange(1.0, K * m + 1)
+    assert np.array_equal(P._chains_start(per, K, m), per)
+    assert np.array_equal(P._chains_start(per.reshape(K, m), K, m), per)
+    for bad in (np.ones(m - 1), np.ones(m + 1), np.ones(2 * m)):
+        with pytest.raises(ValueError):
+            P._chains_start(bad, K, m)
+
+
 def test_stats_len(lib):
     for n in (1, 3, 10, 32):
         assert lib.pht_stats_len(n) == P.stats_len(n) == 2 * n + n * n + 16
@@ -79,13 +96,21 @@ def test_stats_len(lib):
 
 def test_zexp_matches_oracle(lib, orc):
     rng = np.random.default_rng(3)
-    for scale in (1e-3, 1.0, 50.0, 1e6):
-        y = rng.exponential(scale, 10007)
-        assert lib.pht_zexp(y, len(y)) == orc.lib.orc_zexp(y, len(y))
-    # bound: sum(y) * 2^zexp < 2^52, so fixed-point totals never overflow
+    for scale in (1e-12, 1e-10, 1e-3, 1.0, 50.0, 1e6):
+        for N in (1, 200, 10007):
+            y = rng.exponential(scale, N)
+            ze = lib.pht_zexp(y, len(y))
+            assert ze == orc.lib.orc_zexp(y, len(y))
+            # sum(y) * 2^zexp in [2^51, 2^52): totals never overflow, and the
+            # quantum 2^-zexp is ~2^-52 of sum(y) at every time scale
+            assert 2.0 ** 51 <= y.sum() * 2.0 ** ze < 2.0 ** 52, (scale, N)
     y = rng.exponential(2.0, 1_000_000)
     ze = lib.pht_zexp(y, len(y))
-    assert y.sum() * 2.0 ** ze < 2.0 ** 52 and y.sum() * 2.0 ** (ze + 1) >= 2.0 ** 51
+    assert 2.0 ** 51 <= y.sum() * 2.0 ** ze < 2.0 ** 52
+    # degenerate sums: a finite, valid exponent, identical in the oracle
+    for y in (np.zeros(0), np.zeros(5), np.array([np.inf, 1.0]), np.array([np.nan]), np.array([1e-320])):
+        ze = lib.pht_zexp(y, len(y))
+        assert ze == orc.lib.orc_zexp(y, len(y)) and -1000 <= ze <= 1000
 
 
 # --------------------------------------------------- packed parameter block

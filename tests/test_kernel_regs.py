@@ -40,3 +40,15 @@ def test_mhrs_search_occupancy(regs):
     assert len(hits) >= 6 * 6  # 6 round widths x 6 compiled n
     for name, d in hits.items():
         assert d["waves_per_simd"] >= 4 and d["vgpr_spill"] == 0, (name, d)
+
+
+@pytest.mark.parametrize("nt", [3, 5, 10, 15, 20])
+def test_ecs_debug_instantiations(regs, nt):
+    """Informational bound on the DEBUG=true ECS kernels (per-observation
+    outputs; the parity tests run them, nothing times them): they may spill
+    a few VGPRs (n = 15: 6, n = 20: 18 at r01) but must not blow up."""
+    key = f"ecs_exact_kernelILi{nt}ELb1E"
+    hits = {k: v for k, v in regs.items() if key in k}
+    assert len(hits) == 1, (key, list(hits))
+    (name, d), = hits.items()
+    assert d["vgpr_spill"] <= 32, (name, d)
