@@ -83,7 +83,12 @@ def test_time_scale(gpu, orc, method, scale):
         assert np.array_equal(g[f], o[f]), f
     ok = (cen == 0) & (g["flags"] == 0) & (y > 0)
     tot = np.ldexp(g["zq"].sum(axis=1).astype(np.float64), -zexp)
-    assert np.all(np.abs(tot[ok] - y[ok]) <= 1e-12 * y[ok])
+    # each sojourn rounds to half a quantum 2^-zexp ~ 2^-52 sum(y); the old
+    # fixed floor (quantum 2^-51 time units) was ~1e-6 of y at scale 1e-10
+    jumps = g["N"].sum(axis=(1, 2))
+    bound = (jumps + 2) * 2.0 ** -zexp + 1e-13 * y
+    assert np.all(np.abs(tot[ok] - y[ok]) <= bound[ok])
+    assert 2.0 ** -zexp < 1e-14 * y.sum()
 
 
 @pytest.mark.parametrize("method", [1, 2])
