@@ -29,64 +29,91 @@ namespace pht {
 
 constexpr int kRoundCap = 13; /* envelope points handled by the converged code */
 
-/* meet() at compile-time position K of an envelope with `last` = cnt - 1;
- * positions beyond last are left as they are.  Branch-free form of
- * arms_meet (same expressions, selected). */
-template <int K, int CAP, class Env>
-__device__ __forceinline__ void round_meet(Env &e, int last) {
-  /* last <= CAP - 1: neighbours at or beyond CAP are never used */
-  const bool active = (K <= last);
-  const bool il = (K >= 3), ir = (K + 3 <= last), irl = (K >= 1 && K + 1 <= last);
-  const double xk = e.X(K), yk = e.Y(K);
-  double xm1 = 0.0, ym1 = 0.0, xm3 = 0.0, ym3 = 0.0, xp1 = 0.0, yp1 = 0.0, xp3 = 0.0, yp3 = 0.0;
-  if constexpr (K >= 1) { xm1 = e.X(K - 1); ym1 = e.Y(K - 1); }
-  if constexpr (K >= 3) { xm3 = e.X(K - 3); ym3 = e.Y(K - 3); }
-  if constexpr (K + 1 < CAP) { xp1 = e.X(K + 1); yp1 = e.Y(K + 1); }
-  if constexpr (K + 3 < CAP) { xp3 = e.X(K + 3); yp3 = e.Y(K + 3); }
-  double gl = 0.0, gr = 0.0, grl = 0.0, dl = 0.0, dr = 0.0;
-  if constexpr (K >= 3) gl = PHT_DIV((ym1 - ym3), (xm1 - xm3));
-  gr = ir ? PHT_DIV((yp1 - yp3), (xp1 - xp3)) : 0.0;
-  grl = irl ? PHT_DIV((yp1 - ym1), (xp1 - xm1)) : 0.0;
-  if (irl && il && (gl < grl)) gl = gl + (1.0 + 1.0) * (grl - gl);
-  if (irl && ir && (gr > grl)) gr = gr + (1.0 + 1.0) * (grl - gr);
-  if (il && irl) {
-    dr = (gl - grl) * (xp1 - xm1);
-    dr = (dr < kYEps) ? kYEps : dr;
-  }
-  if (ir && irl) {
-    dl = (grl - gr) * (xp1 - xm1);
-    dl = (dl < kYEps) ? kYEps : dl;
-  }
-  double nx = xk, ny = yk;
-  if (il && ir && irl) {
-    nx = PHT_DIV((dl * xp1 + dr * xm1), (dl + dr));
-    ny = PHT_DIV((dl * yp1 + dr * ym1 + dl * dr), (dl + dr));
-  } else if (il && irl) {
-    nx = xp1;
-    ny = yp1 + dr;
-  } else if (ir && irl) {
-    nx = xm1;
-    ny = ym1 + dl;
-  } else if (il) {
-    ny = ym1 + gl * (xk - xm1);
-  } else if (ir) {
-    ny = yp1 - gr * (xp1 - xk);
-  }
-  if (active) {
-    e.sX(K, nx);
-    e.sY(K, ny);
-  }
-}
-
+/*
+ * All intersection points (even positions) of an envelope of at most CAP
+ * points (cnt = last + 1), branch-free, with arms_meet's expressions
+ * (src/arms.c:700-763).  The slopes arms_meet divides for are those of the
+ * segments between consecutive odd (evaluated) points, and each one serves
+ * up to three intersection points: gl at K = gr at K - 4 = grl at K - 2.
+ * They are divided once here (5 divisions at CAP = 13 instead of 3 per
+ * point), and the two divisions of an interior point run only at the
+ * positions that can be interior (K = 4, 6, 8: K >= 3 and K + 3 <= last).
+ * Every value equals arms_meet's bit for bit: gl and grl are the same
+ * quotients; gr is arms_meet's (y_{K+1} - y_{K+3}) / (x_{K+1} - x_{K+3}),
+ * the same quotient with both operands negated, which is exact except for
+ * the sign of a zero slope, restored explicitly.
+ */
 template <int CAP, class Env>
 __device__ __forceinline__ void round_meets(Env &e, int last) {
-  round_meet<0, CAP>(e, last);
-  round_meet<2, CAP>(e, last);
-  round_meet<4, CAP>(e, last);
-  round_meet<6, CAP>(e, last);
-  round_meet<8, CAP>(e, last);
-  if constexpr (CAP > 9) round_meet<10, CAP>(e, last);
-  if constexpr (CAP > 11) round_meet<12, CAP>(e, last);
+  static_assert(CAP % 2 == 1 && CAP >= 5 && CAP <= 13, "converged meets: odd CAP <= 13");
+  constexpr int NO = (CAP - 1) / 2; /* odd positions 1, 3, ..., CAP - 2 */
+  /* sf[m]: slope of odd points m -> m + 1 (positions 2m+1 -> 2m+3), forward
+   * orientation; sb[m]: the same segment in arms_meet's "gr" orientation */
+  double sf[NO - 1], sb[NO - 1];
+  {
+    double xa = e.X(1), ya = e.Y(1);
+#pragma unroll
+    for (int m = 0; m + 1 < NO; m++) {
+      const double xb = e.X(2 * m + 3), yb = e.Y(2 * m + 3);
+      const double q = PHT_DIV((yb - ya), (xb - xa));
+      sf[m] = q;
+      /* (ya - yb) / (xa - xb): = q, but a zero numerator (ya == yb) gives
+       * a zero with the sign of (xa - xb) */
+      sb[m] = (ya == yb && q == 0.0) ? ((xa - xb < 0.0) ? -0.0 : 0.0) : q;
+      xa = xb;
+      ya = yb;
+    }
+  }
+#pragma unroll
+  for (int K = 0; K < CAP; K += 2) {
+    const int mo = K / 2; /* odd index of position K + 1 */
+    const bool active = (K <= last);
+    const bool il = (K >= 3), ir = (K + 3 <= last), irl = (K >= 1 && K + 1 <= last);
+    double xm1 = 0.0, ym1 = 0.0, xp1 = 0.0, yp1 = 0.0;
+    if (K >= 1) { xm1 = e.X(K - 1); ym1 = e.Y(K - 1); }
+    if (K + 1 < CAP) { xp1 = e.X(K + 1); yp1 = e.Y(K + 1); }
+    const double xk = e.X(K), yk = e.Y(K);
+    double gl = 0.0, gr = 0.0, grl = 0.0, dl = 0.0, dr = 0.0;
+    if (K >= 3) gl = sf[mo - 2];
+    if (K + 3 < CAP) gr = ir ? sb[mo] : 0.0;
+    if (K >= 1 && K + 1 < CAP) grl = irl ? sf[mo - 1] : 0.0;
+    if (irl && il && (gl < grl)) gl = gl + (1.0 + 1.0) * (grl - gl);
+    if (irl && ir && (gr > grl)) gr = gr + (1.0 + 1.0) * (grl - gr);
+    if (il && irl) {
+      dr = (gl - grl) * (xp1 - xm1);
+      dr = (dr < kYEps) ? kYEps : dr;
+    }
+    if (ir && irl) {
+      dl = (grl - gr) * (xp1 - xm1);
+      dl = (dl < kYEps) ? kYEps : dl;
+    }
+    double nx = xk, ny = yk;
+    bool done = false;
+    if (K >= 3 && K + 3 <= CAP - 1) { /* interior: possible only here */
+      if (il && ir && irl) {
+        nx = PHT_DIV((dl * xp1 + dr * xm1), (dl + dr));
+        ny = PHT_DIV((dl * yp1 + dr * ym1 + dl * dr), (dl + dr));
+        done = true;
+      }
+    }
+    if (!done) {
+      if (il && irl) {
+        nx = xp1;
+        ny = yp1 + dr;
+      } else if (ir && irl) {
+        nx = xm1;
+        ny = ym1 + dl;
+      } else if (il) {
+        ny = ym1 + gl * (xk - xm1);
+      } else if (ir) {
+        ny = yp1 - gr * (xp1 - xk);
+      }
+    }
+    if (active) {
+      e.sX(K, nx);
+      e.sY(K, ny);
+    }
+  }
 }
 
 /* arms_cumulate over the first CAP positions (cnt <= CAP); the cumulative
