@@ -1,0 +1,404 @@
+/*
+ * pht_dcs_round.h — the DCS sampler (method 4) as a persistent kernel of
+ * jump-converged rounds.
+ *
+ * The path of an observation (dcs() in pht_device.h: LJMA_Hobolth_endState +
+ * LJMA_samplechain_Hobolth + HobCDF + Find02,
+ * src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:11-51,
+ * src/Simulate_AbsCTMC_gt_Hobolth_DCS.c:23-226, src/utility.c:233-338) is a
+ * sequence of jumps (5.4 on average at cfg5-shaped n = 10, up to ~30), each
+ * a set-up (E = e^{lambda x}, the exit test, the next state) and a Brent
+ * search on HobCDF (~11 CDF evaluations).  With one lane per observation
+ * running dcs() to its end, a lane whose path is short idles until the
+ * longest path of its wavefront is done.  Here a loop iteration ("round")
+ * is ONE jump of every lane; a lane whose path ended takes the next
+ * observation at the top of the next round (its end state and start state,
+ * then its first jump in the same round), so a wavefront waits only for the
+ * slowest Brent search of a jump, not for its longest path.  The round's
+ * e^{lambda_i (y - t)} serve both a new observation's end state (t = 0) and
+ * the jump's E.
+ *
+ * Every lane performs exactly dcs()'s operations on exactly its values, in
+ * the same order, and draws the same words: results are bit-identical to
+ * the one-lane kernel and to the oracle's device specification
+ * (oracle/pht_oracle_impl.h, orcD_dcs).  Two hoists keep values unchanged:
+ * the near-equal-eigenvalue test |(lambda_i - S_jj) / S_jj| < 1e-13 (a
+ * per-sweep n x n predicate, computed once per workgroup into LDS) and
+ * HobCDF's factor 1/prob * S_{lastj,j} / Pab (once per jump).
+ */
+#ifndef PHT_DCS_ROUND_H
+#define PHT_DCS_ROUND_H
+
+#include "pht_device.h"
+
+namespace pht {
+
+/* lane phases */
+enum : int { kDcsFree = 0, kDcsSetup = 1, kDcsNew = 3, kDcsDone = 4 };
+
+/* Find02's state between CDF evaluations (src/utility.c:233-338, find02 in
+ * pht_device.h); tol = 0 as dcs() calls it */
+struct BrentSt {
+  double a, b, c, fa, fb, fc;
+  int maxit;
+};
+
+/* find02's loop head, up to the next evaluation point: returns true when
+ * the search is over (root in `root`), false with b advanced (evaluate f(b)) */
+__device__ __forceinline__ bool brent_head(BrentSt &s, double &root) {
+  const double tol = 0.0;
+  if (!(s.maxit--)) { /* while (maxit--) exhausted */
+    root = s.b;
+    return true;
+  }
+  double prev_step = s.b - s.a, tol_act, p, q, new_step;
+  if (fabs(s.fc) < fabs(s.fb)) {
+    s.a = s.b; s.b = s.c; s.c = s.a;
+    s.fa = s.fb; s.fb = s.fc; s.fc = s.fa;
+  }
+  tol_act = 2 * 2.2204460492503131e-16 * fabs(s.b) + tol / 2;
+  new_step = (s.c - s.b) / 2;
+  if (fabs(new_step) <= tol_act || s.fb == (double)0) {
+    root = s.b;
+    return true;
+  }
+  if (fabs(prev_step) >= tol_act && fabs(s.fa) > fabs(s.fb)) {
+    double t1, cb, t2;
+    cb = s.c - s.b;
+    if (s.a == s.c) {
+      t1 = s.fb / s.fa;
+      p = cb * t1;
+      q = 1.0 - t1;
+    } else {
+      q = s.fa / s.fc; t1 = s.fb / s.fc; t2 = s.fb / s.fa;
+      p = t2 * (cb * q * (q - t1) - (s.b - s.a) * (t1 - 1.0));
+      q = (q - 1.0) * (t1 - 1.0) * (t2 - 1.0);
+    }
+    if (p > (double)0) q = -q;
+    else p = -p;
+    if (p < (0.75 * cb * q - fabs(tol_act * q) / 2) && p < fabs(prev_step * q / 2)) new_step = p / q;
+  }
+  if (fabs(new_step) < tol_act) new_step = (new_step > (double)0) ? tol_act : -tol_act;
+  s.a = s.b; s.fa = s.fb;
+  s.b += new_step;
+  return false;
+}
+
+/* find02's loop tail after fb = f(b) */
+__device__ __forceinline__ void brent_tail(BrentSt &s, double fb) {
+  s.fb = fb;
+  if ((s.fb > 0 && s.fc > 0) || (s.fb < 0 && s.fc < 0)) {
+    s.c = s.a;
+    s.fc = s.fa;
+  }
+}
+
+/* per-lane path state between jumps */
+struct DcsLane {
+  int phase;
+  double y, t;
+  int j, lastj, b, njump;
+};
+
+/*
+ * Persistent DCS kernel body.  blk / nblk: this block's claim chunks
+ * (claim_pos).  LDS: parameter block, accumulators, cursor, near masks.
+ */
+template <int NT, bool DEBUG>
+__device__ __forceinline__ void dcs_round_body(const SweepArgs &a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int n = nval<NT>(a.n);
+  const Layout L = make_layout(n);
+  const int pbytes = L.bytes();
+  {
+    const unsigned long long *src = reinterpret_cast<const unsigned long long *>(a.params);
+    PHT_LDS unsigned long long *dst = (PHT_LDS unsigned long long *)smem;
+    for (int k = threadIdx.x; k < pbytes / 8; k += blockDim.x) dst[k] = src[k];
+  }
+  PHT_LDS unsigned char *lsm = (PHT_LDS unsigned char *)smem;
+  PHT_LDS unsigned long long *zq = (PHT_LDS unsigned long long *)(lsm + pbytes);
+  PHT_LDS unsigned long long *xc = zq + n;
+  PHT_LDS unsigned *Bc = (PHT_LDS unsigned *)(xc + kStatExtra);
+  PHT_LDS unsigned *Nc = Bc + n;
+  PHT_LDS int *cursor = (PHT_LDS int *)(Nc + n * n);
+  PHT_LDS unsigned *nearm = (PHT_LDS unsigned *)(cursor + 1);
+  pht_stage_math_tables();
+  for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
+  for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
+  if (threadIdx.x == 0) *cursor = 0;
+  __syncthreads();
+  Par<NT> P;
+  P.d = (const PHT_LDS double *)lsm;
+  P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
+  P.Lr = L;
+  /* near-equal eigenvalue predicate of HobCDF / the set-up's J
+   * (src/Simulate_AbsCTMC_gt_Hobolth_DCS.c:27,139), per state */
+  for (int jj = threadIdx.x; jj < n; jj += blockDim.x) {
+    const double Sjj = P.S(jj, jj);
+    unsigned m = 0u;
+    for (int i = 0; i < n; i++)
+      if (fabs((P.evals(i) - Sjj) / Sjj) < 1e-13) m |= 1u << i;
+    nearm[jj] = m;
+  }
+  __syncthreads();
+
+  Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
+  Lane ln;
+  ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
+  DcsLane st;
+  st.phase = kDcsFree;
+  long pos = 0;
+  unsigned c_obs = 0, c_flag = 0, c_nd = 0, c_jump = 0, c_brent = 0;
+#ifdef PHT_DCS_DIAG
+  /* diagnostic builds: wavefront-level Brent iterations and rounds (the
+   * statistics block's spare words 6 and 7), against the lanes' evaluations
+   * (word 5) and jumps (word 4): the lane utilisation of each loop */
+  unsigned c_witer = 0, c_wround = 0;
+  auto __lane_id_first = [&]() { return __lane_id() == (unsigned)__builtin_ctzll(__ballot(1)); };
+#endif
+  const unsigned blk = blockIdx.x, nblk = gridDim.x;
+
+  /* observation complete: counters, debug rows; the lane is free again */
+  auto finish_obs = [&]() {
+    const uint32_t nd = pht_stream_pos(&ln.r);
+    if (DEBUG) {
+      a.dbg_flags[pos] = ln.flags;
+      a.dbg_ndraw[pos] = nd;
+    }
+    c_obs++;
+    c_flag += ln.flags ? 1u : 0u;
+    c_nd += nd;
+    c_jump += (unsigned)ln.njump;
+    c_brent += (unsigned)ln.nbrent;
+    st.phase = kDcsFree;
+  };
+  /* the head of dcs()'s jump loop (while (t < y) { if (njump++ >= cap) ...) */
+  auto jump_head = [&]() {
+    if (!(st.t < st.y)) { /* the loop condition (t < y always holds after a jump) */
+      finish_obs();
+      return;
+    }
+    if (st.njump++ >= kMaxJumps) {
+      ln.flags |= kFlagJumpCap;
+      finish_obs();
+      return;
+    }
+    st.lastj = st.j;
+    st.phase = kDcsSetup;
+  };
+
+  for (;;) {
+    /* ---- free lanes take the next observation */
+    if (st.phase == kDcsFree) {
+      const long tk = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const long p = claim_pos(tk, blk, nblk);
+      if (p >= a.count) {
+        st.phase = kDcsDone;
+      } else {
+        pos = a.begin + p;
+        pht_stream_init(&ln.r, a.k0, a.k1, a.gid[pos], 0u, a.sweep);
+        ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
+        if (DEBUG) {
+          sk.dz = a.dbg_zq + pos * n;
+          sk.dN = a.dbg_N + pos * n * n;
+          sk.dB = a.dbg_B + pos;
+          sk.dpre = a.dbg_pre + pos;
+        }
+        st.y = a.y[pos];
+        st.t = 0.0;
+        st.phase = kDcsNew;
+      }
+    }
+    const bool act = (st.phase != kDcsDone);
+    if (!__any(act)) break;
+#ifdef PHT_DCS_DIAG
+    if (__lane_id_first()) c_wround++;
+#endif
+    /* one converged Philox block per round (a jump draws at most 3 words,
+     * a new observation 2 more) */
+    if (act) pht_stream_topup(&ln.r);
+
+    /* ---- e^{lambda_i (y - t)} for every lane (converged): this jump's E,
+     * and for a new observation (t = 0) also its end-state vector */
+    double e[PHT_VEC(NT)];
+    if (act) {
+      const double x = st.y - st.t;
+#pragma unroll
+      for (int i = 0; i < n; i++) e[i] = pht_exp_neg(P.evals(i) * x);
+    }
+
+    /* ---- a new observation: end state ~ (pi e^{yS})_b s_b (endState,
+     * src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:11-51), start state,
+     * the jump loop's head */
+    if (st.phase == kDcsNew) {
+      /* (the weights are recomputed in the scan, as dcs() does, instead of
+       * held in registers) */
+      double av[PHT_VEC(NT)];
+#pragma unroll
+      for (int i = 0; i < n; i++) av[i] = P.piQ(i) * e[i];
+      double sum = 0.0;
+#pragma unroll 1
+      for (int k = 0; k < n; k++) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < n; i++) acc = fma(av[i], P.Qinv(i, k), acc);
+        sum += acc * P.s(k);
+      }
+      const double tg = dev_u(ln.r) * sum;
+      double sofar = 0.0;
+      int q = 0;
+#pragma unroll 1
+      for (; q < n; q++) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < n; i++) acc = fma(av[i], P.Qinv(i, q), acc);
+        sofar += acc * P.s(q);
+        if (!(sofar < tg)) break;
+      }
+      if (q == n) {
+        ln.flags |= kFlagScanEnd;
+        q = n - 1;
+      }
+      st.b = q;
+      const double target = dev_u(ln.r);
+      const int B = pistart(P, target, ln.flags);
+      sk.start(B);
+      st.t = 0.0;
+      st.j = B;
+      st.njump = 0;
+      jump_head(); /* t = 0 < y unless y <= 0 */
+    }
+
+    /* ---- one jump of every active lane (dcs()'s loop body) */
+    if (st.phase == kDcsSetup) {
+      const int j = st.j;
+      const double x = st.y - st.t;
+      const double Sjj = P.S(j, j);
+      const unsigned near = nearm[j];
+      const double *E = e; /* this jump's e^{lambda_i x} */
+      double Pab = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) Pab = fma(P.Q(j, i) * E[i], P.Qinv(i, st.b), Pab);
+      bool done = false;
+      if (j == st.b) {
+        if (dev_runif(ln.r, 0.0, 1.0) < pht_exp_neg(Sjj * (st.y - st.t)) / Pab) {
+          sk.z(j, (st.y - st.t));
+          sk.N(j, j);
+          sk.pre(j);
+          finish_obs();
+          done = true;
+        }
+      }
+      if (!done) {
+        double J[PHT_VEC(NT)];
+        {
+          const double es = pht_exp_neg(Sjj * x);
+#pragma unroll
+          for (int i = 0; i < n; i++) {
+            if ((near >> i) & 1u) J[i] = x * E[i];
+            else J[i] = (E[i] - es) / (P.evals(i) - Sjj);
+          }
+        }
+        const int cnt = P.nsuccS(j);
+        double pw[PHT_VEC(NT)];
+        double p_sum = 0.0;
+        for (int q = 0; q < cnt; q++) {
+          const int i = P.succS(j, q);
+          double tmp = 0.0;
+#pragma unroll
+          for (int k = 0; k < n; k++) tmp = fma(P.Q(i, k) * J[k], P.Qinv(k, st.b), tmp);
+          p_sum += pw[q] = P.S(j, i) / Pab * tmp;
+        }
+        const double target = dev_runif(ln.r, 0.0, p_sum);
+        if (!(target > 0.0)) {
+          ln.flags |= kFlagDcsZero;
+          sk.pre(j);
+          finish_obs();
+          done = true;
+        } else {
+          double sofar = 0.0;
+          int q = 0;
+          for (; q < cnt; q++) {
+            sofar += pw[q];
+            if (!(sofar < target)) break;
+          }
+          if (q == cnt) {
+            ln.flags |= kFlagScanEnd;
+            q = cnt - 1;
+          }
+          st.j = P.succS(j, q);
+          const double prob = pw[q];
+          /* HobCDF (src/Simulate_AbsCTMC_gt_Hobolth_DCS.c:23-47):
+           * 1/prob * S_{lastj,j} / Pab * sum_i Q_ji J_i(x) Qb_i - u, its
+           * factor hoisted out of the evaluations (same operations) */
+          const double coef = 1 / prob * P.S(st.lastj, st.j) / Pab;
+          const double u = dev_runif(ln.r, 0.0, 1.0);
+          const int jn = st.j;
+          /* find02(0, y - t, -u, 1 - u, HobCDF, Tol = 0, Maxit = 1000) */
+          BrentSt bs;
+          bs.a = 0.0;
+          bs.b = st.y - st.t;
+          bs.fa = -u;
+          bs.fb = 1.0 - u;
+          bs.c = bs.a;
+          bs.fc = bs.fa;
+          bs.maxit = 1000 + 1;
+          double root;
+          if (bs.fa == 0.0) {
+            root = bs.a;
+          } else if (bs.fb == 0.0) {
+            root = bs.b;
+          } else {
+            while (!brent_head(bs, root)) {
+#ifdef PHT_DCS_DIAG
+              if (__lane_id_first()) c_witer++;
+#endif
+              const double xb = bs.b;
+              const double c1 = st.y - st.t - xb, c0 = Sjj * xb;
+              double tmp = 0.0;
+#pragma unroll
+              for (int i = 0; i < n; i++) {
+                const double ev = P.evals(i), Ei = E[i];
+                double Ji;
+                if ((near >> i) & 1u) Ji = xb * Ei;
+                else Ji = (Ei - pht_exp_neg(c1 * ev + c0)) / (ev - Sjj);
+                tmp = fma(P.Q(jn, i) * Ji, P.Qinv(i, st.b), tmp);
+              }
+              ln.nbrent++;
+              brent_tail(bs, coef * tmp - u);
+            }
+          }
+          double jtime = root;
+          while (st.t + jtime >= st.y) jtime = jtime / 2;
+          sk.N(st.lastj, st.j);
+          sk.z(st.lastj, jtime);
+          st.t += jtime;
+          ln.njump++;
+          jump_head();
+        }
+      }
+    }
+  }
+  lds_add(&xc[0], (unsigned long long)c_obs);
+  lds_add(&xc[2], (unsigned long long)c_flag);
+  lds_add(&xc[3], (unsigned long long)c_nd);
+  lds_add(&xc[4], (unsigned long long)c_jump);
+  lds_add(&xc[5], (unsigned long long)c_brent);
+#ifdef PHT_DCS_DIAG
+  lds_add(&xc[6], (unsigned long long)c_witer);
+  lds_add(&xc[7], (unsigned long long)c_wround);
+#endif
+  __syncthreads();
+  unsigned long long *g = a.stats;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    if (zq[k]) atomicAdd(&g[k], zq[k]);
+    if (Bc[k]) atomicAdd(&g[n + k], (unsigned long long)Bc[k]);
+  }
+  for (int k = threadIdx.x; k < n * n; k += blockDim.x)
+    if (Nc[k]) atomicAdd(&g[2 * n + k], (unsigned long long)Nc[k]);
+  for (int k = threadIdx.x; k < kStatExtra; k += blockDim.x)
+    if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
+}
+
+}  // namespace pht
+#endif

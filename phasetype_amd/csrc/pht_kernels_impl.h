@@ -953,6 +953,40 @@ static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
+}  // namespace pht
+/* needs Sink, SweepArgs, claim_pos and lds_add from above */
+#include "pht_dcs_round.h"
+namespace pht {
+
+/* DCS: converged rounds (pht_dcs_round.h), persistent grid */
+#ifndef PHT_DCS_WAVES
+#define PHT_DCS_WAVES 0
+#endif
+template <int NT>
+constexpr int dcs_waves() {
+  return PHT_DCS_WAVES > 0 ? PHT_DCS_WAVES : 2;
+}
+template <int NT, bool DEBUG>
+__global__ void __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu(dcs_waves<NT>())))
+dcs_round_kernel(SweepArgs a) {
+  dcs_round_body<NT, DEBUG>(a);
+}
+template <int NT, bool DEBUG>
+static hipError_t launch_dcs_round(const SweepArgs &a, hipStream_t st) {
+  static LaunchCfg cfg;
+  const int sm = smem_bytes(a.n) + 4 * a.n; /* + near-equal masks */
+  int occ = 0, cus = 0;
+  if (hipError_t e = launch_config(cfg, (const void *)dcs_round_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
+    return e;
+  long grid = (long)cus * occ;
+  const long want = (a.count + kClaimChunk - 1) / kClaimChunk;
+  if (grid > want) grid = want;
+  if (grid < 1) return hipSuccess;
+  hipLaunchKernelGGL((dcs_round_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
+  return hipGetLastError();
+}
+
 template <int NT>
 static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStream_t st) {
   if (method == kMethodECS && a.cens == nullptr) { /* exact-only range */
@@ -971,7 +1005,10 @@ static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStrea
     if (hipError_t e = launch_mhrs_search<NT>(a, st); e != hipSuccess) return e;
     if (debug) PHT_LAUNCH(kMethodMHRS, true); else PHT_LAUNCH(kMethodMHRS, false);
   } else if (method == kMethodDCS) {
-    return debug ? launch_persist<NT, kMethodDCS, true>(a, st) : launch_persist<NT, kMethodDCS, false>(a, st);
+    static const bool legacy = getenv("PHT_DCS_LEGACY") != nullptr; /* A/B: one lane per observation to its end */
+    if (legacy)
+      return debug ? launch_persist<NT, kMethodDCS, true>(a, st) : launch_persist<NT, kMethodDCS, false>(a, st);
+    return debug ? launch_dcs_round<NT, true>(a, st) : launch_dcs_round<NT, false>(a, st);
   } else {
     return debug ? launch_persist<NT, kMethodECS, true>(a, st) : launch_persist<NT, kMethodECS, false>(a, st);
   }
