@@ -880,7 +880,11 @@ static double ORC_FN(hobcdf)(double x, void *vctx) {
     if (fabs((sp->evals[i] - Sll) / Sll) < 1e-13)
       c->J[i] = x * Ei;
     else
+#if ORC_DEV /* device spec: times the reciprocal 1 / (lambda_i - S_ll) */
+      c->J[i] = (Ei - ORC_EXP_NEG((c->y - c->t - x) * sp->evals[i] + Sll * x)) * (1.0 / (sp->evals[i] - Sll));
+#else
       c->J[i] = (Ei - ORC_EXP_NEG((c->y - c->t - x) * sp->evals[i] + Sll * x)) / (sp->evals[i] - Sll);
+#endif
   }
   double tmp = 0.0;
 #if ORC_DEV
@@ -1009,7 +1013,7 @@ static void ORC_FN(obs_dcs)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_ob
     for (int i = 0; i < n; i++) {
 #if ORC_DEV
       if (fabs((sp->evals[i] - Sjj) / Sjj) < 1e-13) J[i] = x * E[i];
-      else J[i] = (E[i] - ORC_EXP_NEG(Sjj * x)) / (sp->evals[i] - Sjj);
+      else J[i] = (E[i] - ORC_EXP_NEG(Sjj * x)) * (1.0 / (sp->evals[i] - Sjj));
 #else
       if (fabs((sp->evals[i] - Sjj) / Sjj) < 1e-13) J[i] = (y - t) * ORC_EXP_NEG(sp->evals[i] * (y - t));
       else J[i] = (ORC_EXP_NEG(sp->evals[i] * (y - t)) - ORC_EXP_NEG(Sjj * (y - t))) / (sp->evals[i] - Sjj);

@@ -21,10 +21,19 @@
  * Every lane performs exactly dcs()'s operations on exactly its values, in
  * the same order, and draws the same words: results are bit-identical to
  * the one-lane kernel and to the oracle's device specification
- * (oracle/pht_oracle_impl.h, orcD_dcs).  Two hoists keep values unchanged:
- * the near-equal-eigenvalue test |(lambda_i - S_jj) / S_jj| < 1e-13 (a
- * per-sweep n x n predicate, computed once per workgroup into LDS) and
- * HobCDF's factor 1/prob * S_{lastj,j} / Pab (once per jump).
+ * (oracle/pht_oracle_impl.h, orcD_dcs).  Per-sweep n x n tables, computed
+ * once per workgroup into LDS, take the divisions out of the CDF
+ * evaluations: the near-equal-eigenvalue test |(lambda_i - S_jj) / S_jj| <
+ * 1e-13 (same values), and 1 / (lambda_i - S_jj), which the device spec
+ * multiplies by where the reference divides.  HobCDF's
+ * factor 1/prob * S_{lastj,j} / Pab is computed once per jump.
+ *
+ * Measured alternative (not kept): rounds of ONE CDF evaluation per lane
+ * (a lane whose Brent search ends sets up its next jump at once) remove the
+ * wait for the slowest search of a jump (the wavefront's Brent loop runs
+ * 1.65x the mean number of evaluations), but the set-up, end-state and
+ * Brent-step code then runs divergently in every round: 10-18 % slower at
+ * n = 10 and 15 (profiles/r02/dcs/).
  */
 #ifndef PHT_DCS_ROUND_H
 #define PHT_DCS_ROUND_H
@@ -93,6 +102,13 @@ __device__ __forceinline__ void brent_tail(BrentSt &s, double fb) {
   }
 }
 
+/* LDS layout after the sweep kernels' common part (parameter block,
+ * accumulators, cursor): near masks [n] u32, then rinv [n*n] f64 */
+__host__ __device__ constexpr int dcs_rinv_offset(int pbytes, int n) {
+  return (pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 4 * n + 7) & ~7;
+}
+__host__ __device__ constexpr int dcs_smem_bytes(int pbytes, int n) { return dcs_rinv_offset(pbytes, n) + 8 * n * n; }
+
 /* per-lane path state between jumps */
 struct DcsLane {
   int phase;
@@ -122,6 +138,9 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a) {
   PHT_LDS unsigned *Nc = Bc + n;
   PHT_LDS int *cursor = (PHT_LDS int *)(Nc + n * n);
   PHT_LDS unsigned *nearm = (PHT_LDS unsigned *)(cursor + 1);
+  /* rinv[j n + i] = 1 / (lambda_i - S_jj): J's divisor as a reciprocal
+   * (device spec) */
+  PHT_LDS double *rinv = (PHT_LDS double *)(lsm + dcs_rinv_offset(pbytes, n));
   pht_stage_math_tables();
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
@@ -139,6 +158,10 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a) {
     for (int i = 0; i < n; i++)
       if (fabs((P.evals(i) - Sjj) / Sjj) < 1e-13) m |= 1u << i;
     nearm[jj] = m;
+  }
+  for (int k = threadIdx.x; k < n * n; k += blockDim.x) {
+    const int jj = k / n, i = k % n;
+    rinv[k] = 1.0 / (P.evals(i) - P.S(jj, jj));
   }
   __syncthreads();
 
@@ -187,6 +210,59 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a) {
     st.phase = kDcsSetup;
   };
 
+  /* a new observation's end state ~ (pi e^{yS})_b s_b (endState,
+   * src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:11-51) from its
+   * e^{lambda_i y}, start state, and the jump loop's head */
+  auto new_obs = [&](const double *ey) {
+    /* (the weights are recomputed in the scan, as dcs() does, instead of
+     * held in registers) */
+    double av[PHT_VEC(NT)];
+#pragma unroll
+    for (int i = 0; i < n; i++) av[i] = P.piQ(i) * ey[i];
+    double sum = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < n; k++) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) acc = fma(av[i], P.Qinv(i, k), acc);
+      sum += acc * P.s(k);
+    }
+    const double tg = dev_u(ln.r) * sum;
+    double sofar = 0.0;
+    int q = 0;
+#pragma unroll 1
+    for (; q < n; q++) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) acc = fma(av[i], P.Qinv(i, q), acc);
+      sofar += acc * P.s(q);
+      if (!(sofar < tg)) break;
+    }
+    if (q == n) {
+      ln.flags |= kFlagScanEnd;
+      q = n - 1;
+    }
+    st.b = q;
+    const double target = dev_u(ln.r);
+    const int B = pistart(P, target, ln.flags);
+    sk.start(B);
+    st.t = 0.0;
+    st.j = B;
+    st.njump = 0;
+    jump_head(); /* t = 0 < y unless y <= 0 */
+  };
+  /* the end of a jump: find02's root through dcs()'s halving guard, the
+   * statistics, the next loop head */
+  auto end_jump = [&](double root) {
+    double jtime = root;
+    while (st.t + jtime >= st.y) jtime = jtime / 2;
+    sk.N(st.lastj, st.j);
+    sk.z(st.lastj, jtime);
+    st.t += jtime;
+    ln.njump++;
+    jump_head();
+  };
+  {
   for (;;) {
     /* ---- free lanes take the next observation */
     if (st.phase == kDcsFree) {
@@ -230,44 +306,7 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a) {
     /* ---- a new observation: end state ~ (pi e^{yS})_b s_b (endState,
      * src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:11-51), start state,
      * the jump loop's head */
-    if (st.phase == kDcsNew) {
-      /* (the weights are recomputed in the scan, as dcs() does, instead of
-       * held in registers) */
-      double av[PHT_VEC(NT)];
-#pragma unroll
-      for (int i = 0; i < n; i++) av[i] = P.piQ(i) * e[i];
-      double sum = 0.0;
-#pragma unroll 1
-      for (int k = 0; k < n; k++) {
-        double acc = 0.0;
-#pragma unroll
-        for (int i = 0; i < n; i++) acc = fma(av[i], P.Qinv(i, k), acc);
-        sum += acc * P.s(k);
-      }
-      const double tg = dev_u(ln.r) * sum;
-      double sofar = 0.0;
-      int q = 0;
-#pragma unroll 1
-      for (; q < n; q++) {
-        double acc = 0.0;
-#pragma unroll
-        for (int i = 0; i < n; i++) acc = fma(av[i], P.Qinv(i, q), acc);
-        sofar += acc * P.s(q);
-        if (!(sofar < tg)) break;
-      }
-      if (q == n) {
-        ln.flags |= kFlagScanEnd;
-        q = n - 1;
-      }
-      st.b = q;
-      const double target = dev_u(ln.r);
-      const int B = pistart(P, target, ln.flags);
-      sk.start(B);
-      st.t = 0.0;
-      st.j = B;
-      st.njump = 0;
-      jump_head(); /* t = 0 < y unless y <= 0 */
-    }
+    if (st.phase == kDcsNew) new_obs(e);
 
     /* ---- one jump of every active lane (dcs()'s loop body) */
     if (st.phase == kDcsSetup) {
@@ -296,7 +335,7 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a) {
 #pragma unroll
           for (int i = 0; i < n; i++) {
             if ((near >> i) & 1u) J[i] = x * E[i];
-            else J[i] = (E[i] - es) / (P.evals(i) - Sjj);
+            else J[i] = (E[i] - es) * rinv[j * n + i];
           }
         }
         const int cnt = P.nsuccS(j);
@@ -361,23 +400,18 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a) {
                 const double ev = P.evals(i), Ei = E[i];
                 double Ji;
                 if ((near >> i) & 1u) Ji = xb * Ei;
-                else Ji = (Ei - pht_exp_neg(c1 * ev + c0)) / (ev - Sjj);
+                else Ji = (Ei - pht_exp_neg(c1 * ev + c0)) * rinv[j * n + i];
                 tmp = fma(P.Q(jn, i) * Ji, P.Qinv(i, st.b), tmp);
               }
               ln.nbrent++;
               brent_tail(bs, coef * tmp - u);
             }
           }
-          double jtime = root;
-          while (st.t + jtime >= st.y) jtime = jtime / 2;
-          sk.N(st.lastj, st.j);
-          sk.z(st.lastj, jtime);
-          st.t += jtime;
-          ln.njump++;
-          jump_head();
+          end_jump(root);
         }
       }
     }
+  }
   }
   lds_add(&xc[0], (unsigned long long)c_obs);
   lds_add(&xc[2], (unsigned long long)c_flag);

@@ -1018,7 +1018,7 @@ struct HobCdf {
       const double ev = P.evals(i), Ei = E[i];
       double Ji;
       if (fabs((ev - Sll) / Sll) < 1e-13) Ji = x * Ei;
-      else Ji = (Ei - pht_exp_neg((y - t - x) * ev + Sll * x)) / (ev - Sll);
+      else Ji = (Ei - pht_exp_neg((y - t - x) * ev + Sll * x)) * (1.0 / (ev - Sll));
       tmp = fma(P.Q(j, i) * Ji, Qb[i], tmp);
     }
     return 1 / prob * P.S(lastj, j) / Pab * tmp - u;
@@ -1147,7 +1147,7 @@ __device__ __forceinline__ void dcs(const Par<NT> &P, double y, Lane &ln, Sink &
     for (int i = 0; i < n; i++) {
       const double ev = P.evals(i);
       if (fabs((ev - Sjj) / Sjj) < 1e-13) J[i] = x * E[i];
-      else J[i] = (E[i] - pht_exp_neg(Sjj * x)) / (ev - Sjj);
+      else J[i] = (E[i] - pht_exp_neg(Sjj * x)) * (1.0 / (ev - Sjj));
     }
     const int cnt = P.nsuccS(j);
     double pw[PHT_VEC(NT)];

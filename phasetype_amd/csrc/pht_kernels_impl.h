@@ -19,6 +19,7 @@
 #define PHT_KERNELS_IMPL_H
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include <algorithm>
 #include <mutex>
@@ -975,9 +976,10 @@ dcs_round_kernel(SweepArgs a) {
 template <int NT, bool DEBUG>
 static hipError_t launch_dcs_round(const SweepArgs &a, hipStream_t st) {
   static LaunchCfg cfg;
-  const int sm = smem_bytes(a.n) + 4 * a.n; /* + near-equal masks */
+  const int sm = dcs_smem_bytes(make_layout(a.n).bytes(), a.n); /* + near masks, reciprocals */
   int occ = 0, cus = 0;
-  if (hipError_t e = launch_config(cfg, (const void *)dcs_round_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
+  if (hipError_t e = launch_config(cfg, (const void *)dcs_round_kernel<NT, DEBUG>, sm, &occ, &cus);
+      e != hipSuccess)
     return e;
   long grid = (long)cus * occ;
   const long want = (a.count + kClaimChunk - 1) / kClaimChunk;
@@ -985,6 +987,14 @@ static hipError_t launch_dcs_round(const SweepArgs &a, hipStream_t st) {
   if (grid < 1) return hipSuccess;
   hipLaunchKernelGGL((dcs_round_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
   return hipGetLastError();
+}
+/* PHT_DCS_KERNEL=legacy: the one-lane kernel (dcs() to the end), for A/B */
+static bool dcs_legacy() {
+  static const bool v = [] {
+    const char *e = getenv("PHT_DCS_KERNEL");
+    return e && !strcmp(e, "legacy");
+  }();
+  return v;
 }
 
 template <int NT>
@@ -1005,8 +1015,7 @@ static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStrea
     if (hipError_t e = launch_mhrs_search<NT>(a, st); e != hipSuccess) return e;
     if (debug) PHT_LAUNCH(kMethodMHRS, true); else PHT_LAUNCH(kMethodMHRS, false);
   } else if (method == kMethodDCS) {
-    static const bool legacy = getenv("PHT_DCS_LEGACY") != nullptr; /* A/B: one lane per observation to its end */
-    if (legacy)
+    if (dcs_legacy())
       return debug ? launch_persist<NT, kMethodDCS, true>(a, st) : launch_persist<NT, kMethodDCS, false>(a, st);
     return debug ? launch_dcs_round<NT, true>(a, st) : launch_dcs_round<NT, false>(a, st);
   } else {
