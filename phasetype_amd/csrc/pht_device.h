@@ -960,7 +960,7 @@ __device__ __forceinline__ bool mhrs_attempt(const Par<NT> &P, double y, int cen
       t = y;
       break;
     }
-    t = t + dev_rexp(r, 1.0 / -P.S(j, j));
+    t = t + dev_rexp(r, P.scale(j)) /* = 1.0 / -S_jj, per sweep (pht_layout.h) */;
     target = pht_next_u(&r);
     const int cnt = P.nsuccPf(j);
     sofar = 0.0;

@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(kBlock) mhrs_search(SweepArgs a, uint32_t A0, 
           t = y;
           j = n; /* ends the attempt; t >= y: accepted as in mhrs_attempt */
         } else {
-          t = t + dev_rexp(r, 1.0 / -P.S(j, j));
+          t = t + dev_rexp(r, P.scale(j)) /* = 1.0 / -S_jj, per sweep (pht_layout.h) */;
           const double target = pht_next_u(&r);
           const int cnt = P.nsuccPf(j);
           double sofar = 0.0;
