@@ -529,6 +529,7 @@ static int group_sweep(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   ac.cens = c->d_cens;
   ac.begin = c->n_exact;
   ac.count = c->count - c->n_exact;
+  ac.allcens = 1;
   std::unique_lock<std::mutex> lk(g->m);
   memcpy(g->h_params + (size_t)g->pb * w, c->h_params, g->pb);
   g->ex[w] = ae;
@@ -788,6 +789,7 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     SweepArgs ac = a;
     ac.begin = c->n_exact;
     ac.count = c->count - c->n_exact;
+    ac.allcens = 1; /* positions [n_exact, count) hold the censored observations */
     /* both ranges: the censored kernel on stream2, concurrently, so each
      * persistent kernel's tail (its longest paths) fills with the other's
      * work; cfg5 ECS 2.49 -> 1.92 ms; the launch order does not matter

@@ -813,21 +813,42 @@ struct CjDens { /* log F_{P_j}(y - t - d) + log dexp(d; 1/-S_jj) */
   }
 };
 
-template <int NT, class Env, class Sink>
-__device__ __forceinline__ void censored(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
-  const int n = P.n();
-  double target = dev_u(ln.r);
+/* path state of a censored observation between jumps */
+struct CensLane {
+  double y, t, lastt;
+  int j, lastj, njump;
+};
+
+/* start state (LJMA_samplechain, src/Simulate_AbsCTMC_gt_Aslett_DCS.c:315) */
+template <int NT, class Sink>
+__device__ __forceinline__ void censored_begin(const Par<NT> &P, double y, Lane &ln, Sink &sk, CensLane &c) {
+  const double target = dev_u(ln.r);
   const int B = pistart(P, target, ln.flags);
   sk.start(B);
-  double t = 0.0, lastt = 0.0;
-  int j = B, lastj = 0, njump = 0;
-  for (;;) {
-    if (njump++ >= kMaxJumps) {
-      ln.flags |= kFlagJumpCap;
-      break;
-    }
-    lastt = t;
-    lastj = j;
+  c.y = y;
+  c.t = 0.0;
+  c.lastt = 0.0;
+  c.j = B;
+  c.lastj = 0;
+  c.njump = 0;
+}
+
+/* one jump of the censored path (the loop body of LJMA_samplechain,
+ * src/Simulate_AbsCTMC_gt_Aslett_DCS.c:320-388, with LJMA_condjump_r_ars
+ * :184-260); true = the path is complete and recorded */
+template <int NT, class Env, class Sink>
+__device__ __forceinline__ bool censored_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, CensLane &c) {
+  const int n = P.n();
+  const double y = c.y;
+  bool done = false;
+  if (c.njump++ >= kMaxJumps) {
+    ln.flags |= kFlagJumpCap;
+    done = true;
+  } else {
+    const double t = c.t;
+    const int j = c.j;
+    c.lastt = t;
+    c.lastj = j;
     const double Sjj = P.S(j, j);
     double d;
     /* LJMA_condjump_r_ars */
@@ -853,10 +874,13 @@ __device__ __forceinline__ void censored(const Par<NT> &P, double y, Lane &ln, E
         d = xsamp;
       }
     }
-    t += d;
-    target = dev_u(ln.r);
-    if (t < y) {
-      const double x1 = y - t;
+    const int lastj = j;
+    const double tn = t + d;
+    c.t = tn;
+    const double target = dev_u(ln.r);
+    int nj;
+    if (tn < y) {
+      const double x1 = y - tn;
       double E[PHT_VEC(NT)];
 #pragma unroll
       for (int i = 0; i < n; i++) E[i] = pht_exp_neg(P.evals(i) * x1);
@@ -882,7 +906,7 @@ __device__ __forceinline__ void censored(const Par<NT> &P, double y, Lane &ln, E
         ln.flags |= kFlagScanEnd;
         sel = (cnt > 0) ? P.succP(lastj, cnt - 1) : 0;
       }
-      j = sel;
+      nj = sel;
     } else {
       const int cnt = P.nsuccPf(lastj);
       double sofar = 0.0;
@@ -899,16 +923,31 @@ __device__ __forceinline__ void censored(const Par<NT> &P, double y, Lane &ln, E
         ln.flags |= kFlagScanEnd;
         sel = (cnt > 0) ? P.succPf(lastj, cnt - 1) : 0;
       }
-      j = sel;
+      nj = sel;
     }
-    if (j == n) break;
-    sk.z(lastj, t - lastt);
-    sk.N(lastj, j);
-    ln.njump++;
+    c.j = nj;
+    if (nj == n) {
+      done = true;
+    } else {
+      sk.z(lastj, tn - c.lastt);
+      sk.N(lastj, nj);
+      ln.njump++;
+    }
   }
-  sk.z(lastj, t - lastt);
-  sk.pre(lastj);
-  sk.N(lastj, lastj);
+  if (done) {
+    sk.z(c.lastj, c.t - c.lastt);
+    sk.pre(c.lastj);
+    sk.N(c.lastj, c.lastj);
+  }
+  return done;
+}
+
+template <int NT, class Env, class Sink>
+__device__ __forceinline__ void censored(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
+  CensLane c;
+  censored_begin(P, y, ln, sk, c);
+  while (!censored_jump(P, ln, env, sk, c)) {
+  }
 }
 
 /* ================================================================ MHRS */

@@ -33,6 +33,7 @@ struct SweepArgs {
   int spread;                  /* ECS exact: first claims lane-major (the longest paths one per wavefront) */
   int newcap;                  /* ECS exact: observations a lane may start per round (0 = no limit) */
   double hoty;                 /* ECS exact: waves with a path whose remaining time exceeds hoty issue at high priority (0 = off) */
+  int allcens;                 /* ECS: every observation of the launch is right-censored (jump-converged kernel) */
   /* MHRS attempt search (pht_kernels.hip, MHRS section): per chain task
    * (position * (1 + mhit) + c) its first success (attempt << 8 | pre), two
    * task queues and the queue counters; allocated by the host for MHRS */

@@ -957,6 +957,7 @@ static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
 }  // namespace pht
 /* needs Sink, SweepArgs, claim_pos and lds_add from above */
 #include "pht_dcs_round.h"
+#include "pht_cens_round.h"
 namespace pht {
 
 /* DCS: converged rounds (pht_dcs_round.h), persistent grid */
@@ -988,6 +989,36 @@ static hipError_t launch_dcs_round(const SweepArgs &a, hipStream_t st) {
   hipLaunchKernelGGL((dcs_round_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
   return hipGetLastError();
 }
+/* ECS censored range: jump-converged rounds (pht_cens_round.h) */
+template <int NT, bool DEBUG>
+__global__ void __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu(persist_waves<NT, kMethodECS>())))
+cens_round_kernel(SweepArgs a) {
+  cens_round_body<NT, DEBUG>(a);
+}
+template <int NT, bool DEBUG>
+static hipError_t launch_cens_round(const SweepArgs &a, hipStream_t st) {
+  static LaunchCfg cfg;
+  const int sm = smem_bytes(a.n);
+  int occ = 0, cus = 0;
+  if (hipError_t e = launch_config(cfg, (const void *)cens_round_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
+    return e;
+  long grid = (long)cus * occ;
+  const long want = (a.count + kClaimChunk - 1) / kClaimChunk;
+  if (grid > want) grid = want;
+  if (grid < 1) return hipSuccess;
+  hipLaunchKernelGGL((cens_round_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
+  return hipGetLastError();
+}
+/* PHT_CENS_KERNEL=legacy: one lane per censored observation to its end (A/B) */
+static bool cens_legacy() {
+  static const bool v = [] {
+    const char *e = getenv("PHT_CENS_KERNEL");
+    return e && !strcmp(e, "legacy");
+  }();
+  return v;
+}
+
 /* PHT_DCS_KERNEL=legacy: the one-lane kernel (dcs() to the end), for A/B */
 static bool dcs_legacy() {
   static const bool v = [] {
@@ -1019,6 +1050,8 @@ static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStrea
       return debug ? launch_persist<NT, kMethodDCS, true>(a, st) : launch_persist<NT, kMethodDCS, false>(a, st);
     return debug ? launch_dcs_round<NT, true>(a, st) : launch_dcs_round<NT, false>(a, st);
   } else {
+    if (a.allcens && !cens_legacy())
+      return debug ? launch_cens_round<NT, true>(a, st) : launch_cens_round<NT, false>(a, st);
     return debug ? launch_persist<NT, kMethodECS, true>(a, st) : launch_persist<NT, kMethodECS, false>(a, st);
   }
 #undef PHT_LAUNCH
