@@ -654,7 +654,15 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
       break;
     }
     PHT_STAMP(ln, 0);
-    if (!__any(need) && !__any(pend)) break;
+    /* leave only when every lane is done: a lane that hit the newcap of
+     * this round (its new observation ended at its first absorb test) has
+     * its next observation claimed and starts it in the next round, even
+     * when no lane of the wavefront has a sojourn to sample now (r02 fix:
+     * such wavefronts used to leave, dropping those observations) */
+    if (!__any(need) && !__any(pend)) {
+      if (!__any(!done)) break;
+      continue;
+    }
     /* the waves carrying the longest remaining paths issue first, so the
      * sweep's critical path is not slowed by the others */
     if (a.hoty > 0.0) {

@@ -53,6 +53,31 @@ def test_state_counts(gpu, orc, method, n):
 
 
 @pytest.mark.parametrize("method", [1, 2, 4])
+def test_single_state_many_per_lane(gpu, method):
+    """n = 1: every path is its start state until absorption at y (no jump,
+    every absorb test succeeds), so the statistics are known exactly: B = N,
+    N[0,0] = N, zq = sum_i rint(y_i 2^zexp).  300,000 observations give each
+    lane of the persistent ECS grid several, so every wavefront's lanes end
+    their paths in the same round, round after round (r02 fix: the ECS kernel
+    left a wavefront whose lanes had all hit the one-new-observation-per-round
+    cap, dropping their next observations)."""
+    S, s = bd_exit(1)
+    rng = np.random.default_rng(12)
+    N = 300_000
+    y = rng.exponential(1.0, N)
+    cen = np.zeros(N, np.int32)
+    zexp = P.zexp_for(y)
+    sw = P.Sweeper(1, method, 1)
+    sw.set_obs(y, cen)
+    st = sw.sweep(S, s, key=(5, 6), sweep=1, zexp=zexp)
+    sw.close()
+    zq, B, Nt, ex = P.split_stats(st, 1)
+    assert ex[0] == N
+    assert B[0] == N and Nt[0, 0] == N
+    assert zq[0] == int(np.rint(y * 2.0 ** zexp).astype(np.int64).sum())
+
+
+@pytest.mark.parametrize("method", [1, 2, 4])
 def test_zero_and_tiny_times(gpu, orc, method):
     y = np.array([0.0, 1e-300, 1e-12, 1e-6, 0.0, 2.5, 0.0, 1e-9])
     cen = np.array([0, 0, 0, 0, 1, 0, 1, 1], np.int32)
