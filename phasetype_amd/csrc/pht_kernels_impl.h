@@ -548,6 +548,10 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
   ln.st_rounds = 0ull;
 #endif
   EcsLane<NT> st;
+  /* a lane without an observation still runs the converged round code
+   * (its results unused): keep its state index in range */
+  st.j = 0;
+  st.yt = 0.0;
   long pos = 0;
   bool have = false, done = false;
   /* the lane's next observation is claimed and its (y, gid) loaded one
@@ -658,11 +662,11 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
      * this round (its new observation ended at its first absorb test) has
      * its next observation claimed and starts it in the next round, even
      * when no lane of the wavefront has a sojourn to sample now (r02 fix:
-     * such wavefronts used to leave, dropping those observations) */
-    if (!__any(need) && !__any(pend)) {
-      if (!__any(!done)) break;
-      continue;
-    }
+     * such wavefronts used to leave, dropping those observations).  Such a
+     * round runs ecs_round with no lane active (a rare case), which keeps
+     * the loop's single back-edge: a `continue` here changed the register
+     * allocation (n = 10: 285 VGPRs, one wave per SIMD) */
+    if (!__any(need) && !__any(pend) && !__any(!done)) break;
     /* the waves carrying the longest remaining paths issue first, so the
      * sweep's critical path is not slowed by the others */
     if (a.hoty > 0.0) {
