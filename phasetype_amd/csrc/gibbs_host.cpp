@@ -719,6 +719,14 @@ static int exact_occ(const pht_ctx *c) {
   return 0;
 }
 
+/* exact observations (the longest, positions [0, k) of the decreasing-y
+ * order) that run one per 16-lane row (pht_ecs_row.h) instead of one per
+ * lane; PHT_ROWK=k forces k (results are identical for every k) */
+static long exact_rowk(const pht_ctx *c) {
+  if (const char *e = getenv("PHT_ROWK")) return std::max(0L, std::min(atol(e), c->n_exact));
+  return 0;
+}
+
 static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int zexp, bool debug) {
   HIPCHK(hipSetDevice(c->device));
   const int pb = make_layout(c->n).bytes();
@@ -774,6 +782,8 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     ae.cens = nullptr;
     ae.group = exact_group(c);
     ae.occ = exact_occ(c);
+    ae.rowk = exact_rowk(c);
+    ae.rowprio = getenv("PHT_ROWPRIO") ? atoi(getenv("PHT_ROWPRIO")) : 3;
     /* lane-major first claims when the shard is within ~2 observations per
      * lane (the longest paths, one per wavefront; tools/latency.py:
      * -10 % at 31k-125k per GPU); PHT_SPREAD=0|1 forces it */

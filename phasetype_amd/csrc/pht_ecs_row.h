@@ -1,0 +1,561 @@
+/*
+ * pht_ecs_row.h — the ECS-exact path of ONE observation on a 16-lane DPP row.
+ *
+ * Why: with few observations per lane (the benchmark's N = 1e6 over 8 GPUs is
+ * 125k per GPU, about one per lane) the sweep time is the latency of the
+ * longest latent paths: ~50 jumps in sequence, each a serial ARMS chain.  One
+ * lane runs that chain at ~12 cycles per VALU instruction (rocprofv3 of a lone
+ * wavefront).  Here a row of 16 lanes carries one observation
+ * and spreads every step that has parallelism over its lanes:
+ *   - spectral index i lives in lane gray^-1(i) (slot = rl ^ (rl >> 1)): a
+ *     density evaluation is ONE exponential per lane, and pht_dot16's pairwise
+ *     tree is a DPP butterfly (row_mirror, row_half_mirror, quad mirror,
+ *     quad xor 1 pair exactly the slots s, s ^ 8, s ^ 4, s ^ 2, s ^ 1 that
+ *     pht_dot16 adds), so every lane ends with pht_dot16's value;
+ *   - envelope point k lives in lane k (up to kRowCap points): the meets and
+ *     the areas of cumulate run one per lane (neighbours by DPP row shifts);
+ *     the prefix sum of the areas keeps its sequential order (one DPP step
+ *     per point); invert finds its segment with one ballot;
+ *   - the four ARMS starting points' sums and logs run side by side.
+ * Per-observation control state and the random stream are replicated in the
+ * row's 16 lanes, so control flow is uniform within a row; lane 0 alone
+ * records the statistics.  Every observation gets exactly the draws,
+ * evaluations and arithmetic of the one-lane kernel (pht_ecs_round.h), so
+ * results are bit-identical; envelopes beyond kRowCap points continue in the
+ * general one-lane ARMS code (arms_step) on a private copy, as there.
+ *
+ * The host hands the K longest exact observations of a sweep (positions
+ * [0, K) of the decreasing-y order) to the row blocks of the ECS launch
+ * (ecs_exact_kernel, pht_kernels_impl.h); the rest run one per lane.
+ * Reference: LJMA_samplechain_Aslett2 src/Simulate_AbsCTMC_eq_Aslett_ECS.c:205-373,
+ * arms src/arms.c:115-846 (via the one-lane restatement in pht_device.h).
+ */
+#ifndef PHT_ECS_ROW_H
+#define PHT_ECS_ROW_H
+
+#include "pht_device.h"
+#include "pht_env.h"
+
+namespace pht {
+
+constexpr int kRowW = 16;   /* lanes per observation */
+constexpr int kRowCap = 15; /* envelope points held by the row (point k in lane k) */
+template <int NT>
+constexpr bool row_ok() {
+  return NT > 0 && NT <= kRowW;
+}
+
+/* DPP controls (gfx9 family): quad_perm, row shifts, mirrors */
+constexpr int kDppQuadRev = 0x1B;  /* quad_perm [3,2,1,0] */
+constexpr int kDppQuadX1 = 0xB1;   /* quad_perm [1,0,3,2] */
+constexpr int kDppMirror = 0x140;  /* lane l <- lane 15 - l (in the row) */
+constexpr int kDppHalfMirror = 0x141; /* lane l <- lane 7 - l (in each half row) */
+constexpr int dpp_shl(int s) { return 0x100 + s; } /* lane l <- lane l + s */
+constexpr int dpp_shr(int s) { return 0x110 + s; } /* lane l <- lane l - s */
+
+/* out-of-row sources read 0 (bound_ctrl off, old = 0); every caller selects
+ * such lanes away */
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)dpp_i<CTRL>((int)(unsigned)u);
+  const unsigned hi = (unsigned)dpp_i<CTRL>((int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+/* value of lane k of the row (k row-uniform) */
+__device__ __forceinline__ double row_get(double v, int k) { return __shfl(v, k, kRowW); }
+/* the row's 16 bits of a wavefront ballot */
+__device__ __forceinline__ unsigned row_ballot(bool p) {
+  const unsigned long long m = __ballot(p);
+  return (unsigned)(m >> (threadIdx.x & 48u)) & 0xFFFFu;
+}
+
+/* one level of pht_dot16's tree: slots r and r + s (r < s) are added when
+ * r + s < n; both lanes of the pair compute the same value */
+__device__ __forceinline__ double row_level(double v, double o, int slot, int s, int n) {
+  const bool low = (slot & s) == 0;
+  const bool has = (slot & (s - 1)) + s < n;
+  return has ? v + o : (low ? v : o);
+}
+/* pht_dot16 over the row (n <= 16): v = this lane's slot product (0 beyond
+ * n); every lane returns the sum */
+__device__ __forceinline__ double row_sum16(double v, int slot, int n) {
+  v = row_level(v, dpp_d<kDppMirror>(v), slot, 8, n);
+  v = row_level(v, dpp_d<kDppHalfMirror>(v), slot, 4, n);
+  v = row_level(v, dpp_d<kDppQuadRev>(v), slot, 2, n);
+  v = row_level(v, dpp_d<kDppQuadX1>(v), slot, 1, n);
+  return v;
+}
+
+/* lane-constant row data */
+struct RowId {
+  int rl;     /* lane in the row = envelope position */
+  int slot;   /* spectral index of this lane (gray code of rl) */
+  int ix;     /* slot, or 0 beyond n (parameter-block index) */
+  bool sv;    /* slot < n */
+  bool lead;  /* rl == 0: records the statistics */
+  double lam; /* evals(slot) (0 beyond n) */
+  double lammax;
+};
+
+/* per-observation state (replicated; E0 is this lane's slot) */
+struct RowObs {
+  double yt;
+  int j, njump;
+  bool haveE0, haveDen;
+  double den;
+  double E0; /* e^{lambda_slot yt} */
+};
+
+/* the row's envelope: point rl (x, y), count and ymax (replicated) */
+struct RowEnv {
+  double x, y;
+  int cnt;
+  double ymax;
+};
+
+/* EcsDens on a row: log(sum_i W[j,i] e^{lambda_i (y_t - d)}) + S_jj d */
+template <int NT>
+struct RowDens {
+  const RowId &id;
+  int j;
+  double y_t, Sjj;
+  double w;     /* W[j, slot] */
+  double E0;    /* e^{lambda_slot y_t} */
+  double El;    /* slot of the most recent evaluation */
+  double lastd;
+  __device__ __forceinline__ double sum(double e) const { return row_sum16(id.sv ? w * e : 0.0, id.slot, NT); }
+  __device__ __forceinline__ double operator()(double d) {
+    const double x = y_t - d;
+    El = (d == 0.0) ? E0 : (id.sv ? pht_exp_neg(id.lam * x) : 0.0);
+    const double acc = sum(El);
+    lastd = d;
+    return pht_log(acc) + Sjj * d;
+  }
+  /* EcsDens::init4: the four sums (every lane gets all four) */
+  __device__ __forceinline__ void init4(const double xinit[4], double acc[4]) {
+    const double x3 = y_t - xinit[3];
+    if (pht_ecs_init_ok(id.lammax, xinit[0], x3)) {
+      const double F = id.sv ? pht_exp_neg(id.lam * (y_t - xinit[2])) : 0.0;
+      const double T1 = F * F;
+      const double T0 = E0 * pht_exp_taylor(-id.lam * xinit[0]);
+      El = pht_exp_taylor(id.lam * x3);
+      acc[2] = sum(F);
+      acc[1] = sum(T1);
+      acc[0] = sum(T0);
+      acc[3] = sum(El);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        El = id.sv ? pht_exp_neg(id.lam * (y_t - xinit[k])) : 0.0;
+        acc[k] = sum(El);
+      }
+    }
+    lastd = xinit[3];
+  }
+};
+
+/* round_meets on the row: every intersection point (even positions) at once */
+__device__ __forceinline__ void row_meets(RowEnv &e, int rl) {
+  const int last = e.cnt - 1;
+  const int K = rl;
+  /* slope of the segment from this (odd) point to the next odd point */
+  const double xb = dpp_d<dpp_shl(2)>(e.x), yb = dpp_d<dpp_shl(2)>(e.y);
+  const double q = PHT_DIV((yb - e.y), (xb - e.x));
+  const double sb = (e.y == yb && q == 0.0) ? ((e.x - xb < 0.0) ? -0.0 : 0.0) : q;
+  const double glv = dpp_d<dpp_shr(3)>(q), grlv = dpp_d<dpp_shr(1)>(q), grv = dpp_d<dpp_shl(1)>(sb);
+  const double xm1 = dpp_d<dpp_shr(1)>(e.x), ym1 = dpp_d<dpp_shr(1)>(e.y);
+  const double xp1 = dpp_d<dpp_shl(1)>(e.x), yp1 = dpp_d<dpp_shl(1)>(e.y);
+  const bool il = (K >= 3), ir = (K + 3 <= last), irl = (K >= 1 && K + 1 <= last);
+  const double xk = e.x, yk = e.y;
+  double gl = il ? glv : 0.0, gr = ir ? grv : 0.0, grl = irl ? grlv : 0.0, dl = 0.0, dr = 0.0;
+  if (irl && il && (gl < grl)) gl = gl + (1.0 + 1.0) * (grl - gl);
+  if (irl && ir && (gr > grl)) gr = gr + (1.0 + 1.0) * (grl - gr);
+  if (il && irl) {
+    dr = (gl - grl) * (xp1 - xm1);
+    dr = (dr < kYEps) ? kYEps : dr;
+  }
+  if (ir && irl) {
+    dl = (grl - gr) * (xp1 - xm1);
+    dl = (dl < kYEps) ? kYEps : dl;
+  }
+  double nx = xk, ny = yk;
+  if (il && ir && irl) {
+    nx = PHT_DIV((dl * xp1 + dr * xm1), (dl + dr));
+    ny = PHT_DIV((dl * yp1 + dr * ym1 + dl * dr), (dl + dr));
+  } else if (il && irl) {
+    nx = xp1;
+    ny = yp1 + dr;
+  } else if (ir && irl) {
+    nx = xm1;
+    ny = ym1 + dl;
+  } else if (il) {
+    ny = ym1 + gl * (xk - xm1);
+  } else if (ir) {
+    ny = yp1 - gr * (xp1 - xk);
+  }
+  const bool active = ((K & 1) == 0) && (K <= last);
+  e.x = active ? nx : e.x;
+  e.y = active ? ny : e.y;
+}
+
+/* arms_cumulate's ymax: a scan from position 0 with a strict > keeps the
+ * first maximum, skips NaN at positions >= 1 and sticks to a NaN at 0.  As a
+ * total order on (class, value, position) it reduces in any pairing. */
+struct RowMax {
+  double v;
+  int k;  /* position, or >= 64 for points beyond cnt */
+};
+__device__ __forceinline__ int rowmax_cls(const RowMax &a) {
+  if (a.k >= 64) return 0;
+  if (a.v != a.v) return a.k == 0 ? 3 : 1;
+  return 2;
+}
+__device__ __forceinline__ bool rowmax_better(const RowMax &a, const RowMax &b) {
+  const int ca = rowmax_cls(a), cb = rowmax_cls(b);
+  if (ca != cb) return ca > cb;
+  if (ca == 2 && a.v != b.v) return a.v > b.v;
+  return a.k < b.k;
+}
+template <int CTRL>
+__device__ __forceinline__ RowMax rowmax_step(RowMax m) {
+  RowMax o;
+  o.v = dpp_d<CTRL>(m.v);
+  o.k = dpp_i<CTRL>(m.k);
+  return rowmax_better(o, m) ? o : m;
+}
+
+/* round_cumulate on the row: ymax, then this lane's area (segment rl-1 ->
+ * rl) and the prefix sum in position order; returns cum at position rl */
+__device__ __forceinline__ double row_cumulate(RowEnv &e, int rl) {
+  RowMax m;
+  m.v = e.y;
+  m.k = (rl < e.cnt) ? rl : 64 + rl;
+  m = rowmax_step<kDppMirror>(m);
+  m = rowmax_step<kDppHalfMirror>(m);
+  m = rowmax_step<kDppQuadRev>(m);
+  m = rowmax_step<kDppQuadX1>(m);
+  const double ymax = m.v;
+  e.ymax = ymax;
+  const double eyk = expshift(e.y, ymax);
+  const double xp = dpp_d<dpp_shr(1)>(e.x), yp = dpp_d<dpp_shr(1)>(e.y), eyp = dpp_d<dpp_shr(1)>(eyk);
+  const double xk = e.x, yk = e.y;
+  const double lin = 0.5 * (eyk + eyp) * (xk - xp);
+  const double ex = (PHT_DIV((eyk - eyp), (yk - yp))) * (xk - xp);
+  const double a = (xp == xk) ? 0. : ((fabs(yk - yp) < kYEps) ? lin : ex);
+  /* cum_k = cum_{k-1} + a_k, k = 1 .. cnt-1, in order (one step per point) */
+  double cum = 0.;
+#pragma unroll
+  for (int t = 1; t < kRowCap; t++) {
+    if (!__any(t < e.cnt)) break;
+    const double v = dpp_d<dpp_shr(1)>(cum);
+    cum = (rl == t) ? v + a : cum;
+  }
+  return cum;
+}
+
+/* round_invert on the row (cum: this lane's cumulative area) */
+__device__ __forceinline__ void row_invert(const RowEnv &e, double cum, int rl, double prob, WPt &p) {
+  const int last = e.cnt - 1;
+  const double clast = row_get(cum, last);
+  const double u = prob * clast;
+  /* q moves down from last while cum[q-1] > u */
+  const unsigned stop = row_ballot(rl >= 1 && rl <= last - 1 && !(cum > u));
+  const int q = stop ? (31 - __builtin_clz(stop)) + 1 : 1;
+  p.pr = q;
+  const double cr = row_get(cum, q), cl = row_get(cum, q - 1);
+  const double xl = row_get(e.x, q - 1), xr = row_get(e.x, q);
+  const double yr = row_get(e.y, q), yl = row_get(e.y, q - 1);
+  const double prop = PHT_DIV((u - cl), (cr - cl));
+  const double eyr = expshift(yr, e.ymax);
+  if (xl == xr) {
+    p.x = xr; p.y = yr; p.ey = eyr;
+    return;
+  }
+  const double eyl = expshift(yl, e.ymax);
+  if (fabs(yr - yl) < kYEps) {
+    if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
+      p.x = xl + (PHT_DIV((xr - xl), (eyr - eyl))) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
+    else
+      p.x = xl + (xr - xl) * prop;
+    p.ey = (PHT_DIV((p.x - xl), (xr - xl))) * (eyr - eyl) + eyl;
+    p.y = logshift(p.ey, e.ymax);
+  } else {
+    p.x = xl + (PHT_DIV((xr - xl), (yr - yl))) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
+    p.y = (PHT_DIV((p.x - xl), (xr - xl))) * (yr - yl) + yl;
+    p.ey = expshift(p.y, e.ymax);
+  }
+}
+
+/* round_insert on the row (cnt + 2 <= kRowCap) */
+template <int NT>
+__device__ __forceinline__ void row_insert(RowEnv &e, const ArmsPend &pd, RowDens<NT> &f, Lane &ln, int rl) {
+  const int pr = pd.pr, last = e.cnt - 1;
+  const double xs = dpp_d<dpp_shr(2)>(e.x), ys = dpp_d<dpp_shr(2)>(e.y);
+  const bool mv = (rl >= 2) && (rl - 2 >= pr) && (rl - 2 <= last);
+  e.x = mv ? xs : e.x;
+  e.y = mv ? ys : e.y;
+  e.cnt += 2;
+  const int qi = ((pr - 1) & 1) ? pr + 1 : pr;
+  e.x = (rl == qi) ? pd.px : e.x;
+  e.y = (rl == qi) ? pd.py : e.y;
+  const int ql = (qi >= 2) ? qi - 2 : qi - 1;
+  const int qr = (qi + 2 <= e.cnt - 1) ? qi + 2 : qi + 1;
+  const double xl = row_get(e.x, ql), xr = row_get(e.x, qr);
+  bool adj = false;
+  double xn = 0.0;
+  if (pd.px < (1. - kXEps) * xl + kXEps * xr) {
+    xn = (1. - kXEps) * xl + kXEps * xr;
+    adj = true;
+  } else if (pd.px > kXEps * xl + (1. - kXEps) * xr) {
+    xn = kXEps * xl + (1. - kXEps) * xr;
+    adj = true;
+  }
+  if (adj) {
+    const double yn = f(xn);
+    ln.neval++;
+    e.x = (rl == qi) ? xn : e.x;
+    e.y = (rl == qi) ? yn : e.y;
+  }
+}
+
+/* round_metropolis on the row */
+__device__ __forceinline__ double row_metropolis(const RowEnv &e, int rl, const WPt &p, double ynew, double xprev,
+                                                 double yprev, Lane &ln) {
+  /* ql: while (X(ql + 1) < xprev) ql++ */
+  const unsigned stop = row_ballot(rl >= 1 && !(e.x < xprev));
+  const int ql = stop ? __builtin_ctz(stop) - 1 : kRowW - 2;
+  const int qr = ql + 1;
+  const double xql = row_get(e.x, ql), yql = row_get(e.y, ql);
+  const double xqr = row_get(e.x, qr), yqr = row_get(e.y, qr);
+  double w = PHT_DIV((xprev - xql), (xqr - xql));
+  double zold = yql + w * (yqr - yql);
+  double znew = p.y;
+  if (yprev < zold) zold = yprev;
+  if (ynew < znew) znew = ynew;
+  w = ynew - znew - yprev + zold;
+  if (w > 0.0) w = 0.0;
+  w = (w > -kYCeil) ? pht_exp_core(w) : 0.0;
+  const double um = dev_u(ln.r);
+  return (um > w) ? xprev : p.x;
+}
+
+/* absorb test (ecs_try_absorb); true = path complete and recorded */
+template <int NT, class Sink>
+__device__ __forceinline__ bool row_try_absorb(const Par<NT> &P, const RowId &id, Lane &ln, Sink &sk, RowObs &st) {
+  const int j = st.j;
+  bool fin = false;
+  if (st.njump >= kMaxJumps) {
+    ln.flags |= kFlagJumpCap;
+    fin = true;
+  } else if (P.s(j) > 0.0) {
+    const double y_t = st.yt;
+    const double U = dev_u(ln.r);
+    if (!st.haveE0) {
+      st.E0 = id.sv ? pht_exp_neg(id.lam * y_t) : 0.0;
+      st.haveE0 = true;
+      st.haveDen = false;
+    }
+    const double den = st.haveDen ? st.den : row_sum16(id.sv ? P.QQs(j, id.ix) * st.E0 : 0.0, id.slot, NT);
+    const double pab = pht_exp(fma(P.S(j, j), y_t, P.logs(j)) - pht_log(den));
+    fin = (U < pab);
+  }
+  if (fin && id.lead) {
+    sk.N(j, j);
+    sk.z(j, st.yt);
+    sk.pre(j);
+  }
+  return fin;
+}
+
+/* ecs_jump_finish: moveMass + categorical + statistics */
+template <int NT, class Sink>
+__device__ __forceinline__ void row_jump_finish(const Par<NT> &P, const RowId &id, Lane &ln, Sink &sk, RowObs &st,
+                                                const RowDens<NT> &f, double xsamp, int ainfo) {
+  const int j = st.j;
+  const double y_t = st.yt;
+  if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
+  const double d = xsamp;
+  const double x = y_t - d;
+  if (d == f.lastd) {
+    st.E0 = f.El;
+  } else if (d == 0.0) {
+    /* E0 already holds e^{lambda y_t} */
+  } else {
+    st.E0 = id.sv ? pht_exp_neg(id.lam * x) : 0.0;
+  }
+  st.yt = x;
+  st.haveE0 = true;
+  const int cnt = P.nsuccP(j);
+  double w[NT], accs[NT];
+  double sum = 0.0;
+#pragma unroll
+  for (int q = 0; q < NT; q++) {
+    if (q < cnt) {
+      const int k = P.succP(j, q);
+      accs[q] = row_sum16(id.sv ? P.QQs(k, id.ix) * st.E0 : 0.0, id.slot, NT);
+      w[q] = P.P(j, k) * accs[q];
+      sum += w[q];
+    }
+  }
+  const double target = dev_u(ln.r) * sum;
+  int nj;
+  {
+    double sofar = 0.0;
+    int sel = -1;
+#pragma unroll
+    for (int q = 0; q < NT; q++) {
+      if (q < cnt && sel < 0) {
+        sofar += w[q];
+        if (!(sofar < target)) sel = q;
+      }
+    }
+    if (sel < 0) {
+      ln.flags |= kFlagScanEnd;
+      sel = cnt - 1;
+    }
+    nj = (cnt > 0) ? P.succP(j, sel) : 0;
+    double dsel = 0.0;
+#pragma unroll
+    for (int q = 0; q < NT; q++) dsel = (q == sel) ? accs[q] : dsel;
+    st.den = dsel;
+    st.haveDen = (cnt > 0);
+  }
+  if (id.lead) {
+    sk.z(j, d);
+    sk.N(j, nj);
+  }
+  ln.njump++;
+  st.njump++;
+  st.j = nj;
+}
+
+/*
+ * One ARMS round of a row (ecs_round).  start: begin a jump at st.j; pend:
+ * continue one.  bigm: the jump's envelope outgrew kRowCap and continues in
+ * the general one-lane code on the private copy benv (every lane of the row
+ * runs it, replicated).
+ */
+template <int NT, class Sink>
+__device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lane &ln, RowEnv &ev, EnvPrivate &benv,
+                                          Sink &sk, RowObs &st, bool start, bool &pend, bool &bigm, ArmsPend &pd) {
+  const int rl = id.rl;
+  const double y_t = st.yt;
+  if (start && !st.haveE0) {
+    st.E0 = id.sv ? pht_exp_neg(id.lam * y_t) : 0.0;
+    st.haveE0 = true;
+    st.haveDen = false;
+  }
+  const int j = st.j;
+  RowDens<NT> f{id, j, y_t, P.S(j, j), id.sv ? P.W(j, id.ix) : 0.0, st.E0, 0.0, -1.0};
+  double xsamp = 0.0;
+  int ainfo = 0;
+  bool fin = false;
+  /* ---- starting rows: initial envelope (4 evaluations side by side) */
+  if (start) {
+    double xinit[4];
+    xinit[0] = (y_t) / 1e6;
+    xinit[1] = (y_t) / 3.0;
+    xinit[2] = xinit[1] * 2.0;
+    xinit[3] = y_t - xinit[0];
+    if ((xinit[0] <= 0.0) || (xinit[3] >= y_t)) {
+      ainfo = 1003;
+      fin = true;
+    } else if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) {
+      ainfo = 1004;
+      fin = true;
+    } else {
+      double acc[4];
+      f.init4(xinit, acc);
+      ln.neval += 4;
+      ev.cnt = 9;
+      /* lanes 1, 3, 5, 7: the starting points; 0 and 8: the interval ends */
+      const int k = (rl >> 1) & 3;
+      const double xk = (k == 0) ? xinit[0] : (k == 1) ? xinit[1] : (k == 2) ? xinit[2] : xinit[3];
+      const double ak = (k == 0) ? acc[0] : (k == 1) ? acc[1] : (k == 2) ? acc[2] : acc[3];
+      const bool odd = (rl & 1) && rl < 8;
+      const double yk = pht_log(ak) + f.Sjj * xk;
+      ev.x = (rl == 0) ? 0.0 : (odd ? xk : ((rl == 8) ? y_t : ev.x));
+      ev.y = odd ? yk : ev.y;
+    }
+  }
+  /* ---- pending rows: the update ending the rejected iteration */
+  if (pend && !bigm && ev.cnt + 2 > kRowCap) {
+    /* hand the envelope to the general code (private copy in every lane) */
+    benv.cnt = ev.cnt;
+    benv.ymax = ev.ymax;
+    for (int k = 0; k < ev.cnt; k++) {
+      benv.sX(k, row_get(ev.x, k));
+      benv.sY(k, row_get(ev.y, k));
+    }
+    bigm = true;
+  }
+  const bool big = pend && bigm;
+  if (pend && !big) row_insert<NT>(ev, pd, f, ln, rl);
+  const bool arm = (start && !fin) || (pend && !big);
+  double cum = 0.0;
+  if (arm) {
+    row_meets(ev, rl);
+    cum = row_cumulate(ev, rl);
+  }
+  if (start && !fin) {
+    pd.yprev = f(0.0); /* xprev = 0 lies in [xl, xr] = [0, y_t] */
+    ln.neval++;
+    pd.it = 0;
+  }
+  /* the iteration cap is checked after the update (arms_loop) */
+  if (pend && !big && pd.it >= kArmsMaxIt) {
+    ainfo = 4;
+    fin = true;
+  }
+  bool acc = false;
+  const bool itr = arm && !fin;
+  if (itr) {
+    WPt q;
+    const double pu = dev_u(ln.r);
+    row_invert(ev, cum, rl, pu, q);
+    const double u = dev_u(ln.r) * q.ey;
+    const double yv = logshift(u, ev.ymax);
+    const double ynew = f(q.x);
+    ln.neval++;
+    if (yv >= ynew) {
+      pd.px = q.x; pd.py = ynew; pd.pey = expshift(ynew, ev.ymax); pd.pr = q.pr;
+      pd.it++;
+      pend = true;
+    } else {
+      xsamp = row_metropolis(ev, rl, q, ynew, 0.0, pd.yprev, ln);
+      acc = true;
+    }
+  }
+  /* ---- rare: envelopes beyond kRowCap, one-lane code on the private copy */
+  if (big) {
+    double E0f[NT];
+#pragma unroll
+    for (int i = 0; i < NT; i++) E0f[i] = row_get(st.E0, i ^ (i >> 1) ^ (i >> 2) ^ (i >> 3));
+    EcsDens<NT> f1{P, j, y_t, P.S(j, j), E0f, true, -1.0, {}, 0.0, {}};
+    f1.load(id.lammax);
+    const int rc = arms_step(benv, f1, pd, 0.0, xsamp, ln);
+    if (rc != 1) {
+      ainfo = rc;
+      acc = true;
+      bigm = false;
+      f.lastd = f1.lastd;
+      double v = 0.0;
+#pragma unroll
+      for (int i = 0; i < NT; i++) v = (i == id.slot) ? f1.Elast[i] : v;
+      f.El = v;
+    }
+  }
+  if (acc || fin) {
+    pend = false;
+    row_jump_finish<NT>(P, id, ln, sk, st, f, xsamp, ainfo);
+  }
+}
+
+}  // namespace pht
+#endif

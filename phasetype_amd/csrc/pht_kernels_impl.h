@@ -27,6 +27,7 @@
 #include "pht_device.h"
 #include "pht_ecs_round.h"
 #include "pht_ecs_group.h"
+#include "pht_ecs_row.h"
 #include "pht_env.h"
 #include "pht_kernels.h"
 
@@ -706,6 +707,139 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
     if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
 }
 
+/*
+ * The longest exact observations, one per 16-lane row (pht_ecs_row.h):
+ * positions [0, a.rowk) of the launch range (decreasing y), block b of the
+ * nblk row blocks taking positions b, b + nblk, ... through its LDS cursor.
+ * The row waves issue at raised priority: they carry the sweep's critical
+ * path while one-lane blocks share their CUs.
+ */
+template <int NT, bool DEBUG>
+__device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  constexpr int n = NT;
+  const Layout L = make_layout(n);
+  const int pbytes = L.bytes();
+  {
+    const unsigned long long *src = reinterpret_cast<const unsigned long long *>(a.params);
+    PHT_LDS unsigned long long *dst = (PHT_LDS unsigned long long *)smem;
+    for (int k = threadIdx.x; k < pbytes / 8; k += blockDim.x) dst[k] = src[k];
+  }
+  PHT_LDS unsigned char *lsm = (PHT_LDS unsigned char *)smem;
+  PHT_LDS unsigned long long *zq = (PHT_LDS unsigned long long *)(lsm + pbytes);
+  PHT_LDS unsigned long long *xc = zq + n;
+  PHT_LDS unsigned *Bc = (PHT_LDS unsigned *)(xc + kStatExtra);
+  PHT_LDS unsigned *Nc = Bc + n;
+  PHT_LDS int *cursor = (PHT_LDS int *)(Nc + n * n);
+  pht_stage_math_tables();
+  for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
+  for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
+  if (threadIdx.x == 0) *cursor = 0;
+  __syncthreads();
+  switch (a.rowprio) { /* s_setprio takes an immediate */
+    case 0: break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+  }
+
+  Par<NT> P;
+  P.d = (const PHT_LDS double *)lsm;
+  P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
+  P.Lr = L;
+  RowId id;
+  id.rl = (int)(threadIdx.x & (kRowW - 1));
+  id.slot = id.rl ^ (id.rl >> 1);
+  id.sv = id.slot < n;
+  id.ix = id.sv ? id.slot : 0;
+  id.lead = (id.rl == 0);
+  id.lam = id.sv ? P.evals(id.ix) : 0.0;
+  id.lammax = lam_max(P);
+  Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
+  Lane ln;
+  RowObs st;
+  st.yt = 0.0; st.j = 0; st.njump = 0; st.haveE0 = false; st.haveDen = false; st.den = 0.0; st.E0 = 0.0;
+  RowEnv ev;
+  ev.x = 0.0; ev.y = 0.0; ev.cnt = 0; ev.ymax = 0.0;
+  EnvPrivate benv;
+  ArmsPend pd;
+  bool pend = false, bigm = false;
+  long pos = 0;
+  bool have = false, done = false;
+  unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
+  for (;;) {
+    bool need = false;
+    if (have && !pend) pht_stream_topup(&ln.r);
+    while (!done && !pend) {
+      if (!have) {
+        int t = 0;
+        if (id.lead) t = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        t = __shfl(t, 0, kRowW);
+        const long p = (long)t * nblk + blk;
+        if (p >= a.rowk) {
+          done = true;
+          break;
+        }
+        pos = a.begin + p;
+        pht_stream_init(&ln.r, a.k0, a.k1, a.gid[pos], 0u, a.sweep);
+        ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
+        if (DEBUG) {
+          sk.dz = a.dbg_zq + pos * n;
+          sk.dN = a.dbg_N + pos * n * n;
+          sk.dB = a.dbg_B + pos;
+          sk.dpre = a.dbg_pre + pos;
+        }
+        /* ecs_begin */
+        const double target = dev_u(ln.r);
+        const int B = pistart(P, target, ln.flags);
+        if (id.lead) sk.start(B);
+        st.yt = a.y[pos];
+        st.j = B;
+        st.njump = 0;
+        st.haveE0 = false;
+        st.haveDen = false;
+        have = true;
+      }
+      if (row_try_absorb<NT>(P, id, ln, sk, st)) {
+        const uint32_t nd = pht_stream_pos(&ln.r);
+        if (id.lead) {
+          if (DEBUG) {
+            a.dbg_flags[pos] = ln.flags;
+            a.dbg_ndraw[pos] = nd;
+          }
+          c_obs++;
+          c_neval += ln.neval;
+          c_flag += ln.flags ? 1u : 0u;
+          c_nd += nd;
+          c_jump += ln.njump;
+        }
+        have = false;
+        continue;
+      }
+      need = true;
+      break;
+    }
+    if (!__any(need) && !__any(pend) && !__any(!done)) break;
+    if (need || pend) pht_stream_topup(&ln.r);
+    row_round<NT>(P, id, ln, ev, benv, sk, st, need, pend, bigm, pd);
+  }
+  lds_add(&xc[0], (unsigned long long)c_obs);
+  lds_add(&xc[1], (unsigned long long)c_neval);
+  lds_add(&xc[2], (unsigned long long)c_flag);
+  lds_add(&xc[3], (unsigned long long)c_nd);
+  lds_add(&xc[4], (unsigned long long)c_jump);
+  __syncthreads();
+  unsigned long long *g = a.stats;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    if (zq[k]) atomicAdd(&g[k], zq[k]);
+    if (Bc[k]) atomicAdd(&g[n + k], (unsigned long long)Bc[k]);
+  }
+  for (int k = threadIdx.x; k < n * n; k += blockDim.x)
+    if (Nc[k]) atomicAdd(&g[2 * n + k], (unsigned long long)Nc[k]);
+  for (int k = threadIdx.x; k < kStatExtra; k += blockDim.x)
+    if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
+}
+
 /* waves per SIMD the ECS kernel is compiled for: two at n = 15, where the
  * W row read from LDS (EcsDens) lets it fit (255 VGPRs, no spills, per the
  * built library's metadata: tools/kernel_regs.py); otherwise what the
@@ -720,7 +854,19 @@ template <int NT, bool DEBUG>
 __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(ecs_waves<NT>())))
 ecs_exact_kernel(SweepArgs a) {
-  ecs_exact_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
+  unsigned blk = blockIdx.x, nblk = gridDim.x;
+  if constexpr (row_ok<NT>()) {
+    /* blocks [0, rowblk): the a.rowk longest observations, one per row */
+    if (blk < (unsigned)a.rowblk) {
+      ecs_row_body<NT, DEBUG>(a, blk, (unsigned)a.rowblk);
+      return;
+    }
+    blk -= (unsigned)a.rowblk;
+    nblk -= (unsigned)a.rowblk;
+    a.begin += a.rowk;
+    a.count -= a.rowk;
+  }
+  ecs_exact_body<NT, DEBUG>(a, blk, nblk);
 }
 
 /*
@@ -749,14 +895,20 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
   int occ = 0, cus = 0;
   if (hipError_t e = launch_config(cfg, (const void *)ecs_exact_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
     return e;
-  long want = (a.count + kBlock - 1) / kBlock;
+  /* the rowk longest observations on 16-lane rows (kBlock / kRowW per
+   * block), ahead of the one-lane blocks in the same launch */
+  SweepArgs b = a;
+  b.rowk = row_ok<NT>() ? std::max(0L, std::min(a.rowk, a.count)) : 0;
+  b.rowblk = (int)((b.rowk + (kBlock / kRowW) - 1) / (kBlock / kRowW));
+  long want = (a.count - b.rowk + kBlock - 1) / kBlock;
   /* blocks per CU: the occupancy limit, or fewer (a.occ) when the shard is
    * small and the longest paths, not throughput, set the time */
   const int bpc = (a.occ > 0 && a.occ < occ) ? a.occ : occ;
-  long grid = (long)cus * bpc;
+  long grid = (long)cus * bpc - b.rowblk;
   if (grid > want) grid = want;
-  if (grid < 1) return hipSuccess;
-  hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
+  if (grid < 0) grid = 0;
+  if (grid + b.rowblk < 1) return hipSuccess;
+  hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG>), dim3((unsigned)(grid + b.rowblk)), dim3(kBlock), sm, st, b);
   return hipGetLastError();
 }
 

@@ -212,6 +212,56 @@ def test_longest_paths_bitexact(gpu, orc, monkeypatch, group):
         assert np.array_equal(g["N"], o["N"])
 
 
+@pytest.mark.parametrize("rowk,n,cf", [(10 ** 9, 10, 0.0), (300, 10, 0.3), (10 ** 9, 3, 0.3), (10 ** 9, 5, 0.0),
+                                        (777, 15, 0.3), (1, 10, 0.0)])
+def test_row_kernel_bitexact(gpu, orc, monkeypatch, rowk, n, cf):
+    """The longest exact observations on 16-lane DPP rows (pht_ecs_row.h,
+    PHT_ROWK=k: positions [0, k) of the decreasing-y order; 10**9 = every
+    exact observation) give the oracle's device-spec results bit for bit,
+    per observation, next to the one-lane blocks of the same launch."""
+    monkeypatch.setenv("PHT_ROWK", str(rowk))
+    S0, s0 = bd_exit(n)
+    y, cen = simulate_ph(S0, s0, 3000, seed=3000 + n, censor_frac=cf)
+    S, s = _perturbed(n, n + 2)
+    zexp = int(orc.lib.orc_zexp(np.ascontiguousarray(y), len(y)))
+    o = orc.dev_sweep(2, S, s, y, cen, key=(13, 17), sweep=5, zexp=zexp)
+    sw = P.Sweeper(n, 2, 1)
+    sw.set_obs(y, cen)
+    g = sw.sweep_debug(S, s, key=(13, 17), sweep=5, zexp=zexp)
+    for f in ("B", "pre", "flags", "ndraw"):
+        bad = np.nonzero(g[f] != o[f])[0]
+        assert bad.size == 0, f"{f} differs at obs {bad[:5]}: gpu {g[f][bad[:5]]} oracle {o[f][bad[:5]]}"
+    assert np.array_equal(g["zq"], o["zq"]) and np.array_equal(g["N"], o["N"])
+    st = sw.sweep(S, s, key=(13, 17), sweep=5, zexp=zexp)
+    assert np.array_equal(st[:2 * n + n * n], g["stats"][:2 * n + n * n])
+    _, _, _, ex = P.split_stats(st, n)
+    assert ex[0] == len(y)
+
+
+def test_row_kernel_longest_paths(gpu, orc, monkeypatch):
+    """The 4096 longest of 1e6 paths (envelopes that outgrow the row's 15
+    points and continue in the general ARMS code) all on rows, per
+    observation against the oracle, for three (key, sweep) pairs."""
+    monkeypatch.setenv("PHT_ROWK", "4096")
+    n = 10
+    S0, s0 = bd_exit(n)
+    y, cen = simulate_ph(S0, s0, 1_000_000, seed=4242)
+    idx = np.sort(np.argsort(-y)[:4096])
+    y, cen = np.ascontiguousarray(y[idx]), np.ascontiguousarray(cen[idx])
+    zexp = int(orc.lib.orc_zexp(np.ascontiguousarray(y), len(y)))
+    sw = P.Sweeper(n, 2, 1)
+    sw.set_obs(y, cen)
+    for key, sweep in (((5, 6), 2), ((3, 4), 1), ((9, 1), 7)):
+        o = orc.dev_sweep(2, S0, s0, y, cen, key=key, sweep=sweep, zexp=zexp)
+        g = sw.sweep_debug(S0, s0, key=key, sweep=sweep, zexp=zexp)
+        bad = np.nonzero((g["ndraw"] != o["ndraw"]) | np.any(g["zq"] != o["zq"], axis=1))[0]
+        assert len(bad) == 0, (f"{len(bad)} observations differ, first {bad[:5]}: ndraw gpu "
+                               f"{g['ndraw'][bad[:5]]} oracle {o['ndraw'][bad[:5]]} flags {g['flags'][bad[:5]]}")
+        for f in ("B", "pre", "flags"):
+            assert np.array_equal(g[f], o[f]), f
+        assert np.array_equal(g["N"], o["N"])
+
+
 @pytest.mark.parametrize("launch", ["one", "streams"])
 @pytest.mark.parametrize("method,n,cf", [(2, 5, 0.3), (2, 10, 0.0), (1, 3, 0.3), (4, 3, 0.0)])
 def test_chains_equal_single_runs(gpu, method, n, cf, launch, monkeypatch):

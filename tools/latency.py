@@ -2,7 +2,8 @@
 """Kernel time of the ECS-exact sweep against the shard size (strong-scaling
 regime) for the launch variants the host can pick at run time:
 PHT_GROUP (lanes per observation), PHT_ECS_OCC (blocks per CU), PHT_HOT
-(variant hotK: wave priority for the K longest remaining paths), base = defaults.
+(variant hotK: wave priority for the K longest remaining paths), PHT_ROWK (variant rowK:
+the K longest observations on 16-lane rows), base = defaults.
 
 usage (GPU box): python3 tools/latency.py [--Ns 62500 125000 ...] [--sweeps 8]
 Shard = the first N observations of the bench data set (what rank 0 of
@@ -42,6 +43,10 @@ def main():
         if spec.startswith("rand"):
             k = int(spec[4:])
             idx = np.sort(np.random.default_rng(11).choice(len(y), k, replace=False))
+        elif spec.startswith("drop"):  # dropKofS: the first S observations without their K largest
+            k, sz = (int(v) for v in spec[4:].split("of"))
+            first = np.arange(sz)
+            idx = np.sort(first[np.argsort(-y[:sz])[k:]])
         elif spec.startswith("top"):
             k = int(spec[3:])
             idx = np.sort(np.argsort(-y)[:k])
@@ -58,8 +63,15 @@ def main():
             os.environ.pop("PHT_SPREAD", None)
             os.environ.pop("PHT_NEWCAP", None)
             os.environ.pop("PHT_HOT", None)
+            os.environ.pop("PHT_ROWK", None)
+            os.environ.pop("PHT_ROWPRIO", None)
             if v == "base":
                 pass
+            elif v.startswith("row"):  # rowK[pP]: the K longest observations on 16-lane rows (wave priority P)
+                k, _, pr = v[3:].partition("p")
+                os.environ["PHT_ROWK"] = k
+                if pr:
+                    os.environ["PHT_ROWPRIO"] = pr
             elif v.startswith("hot"):  # waves with one of the K longest remaining paths at high priority
                 os.environ["PHT_HOT"] = v[3:]
             elif v.startswith("nc"):
