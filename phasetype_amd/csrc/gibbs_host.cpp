@@ -724,6 +724,15 @@ static int exact_occ(const pht_ctx *c) {
  * lane; PHT_ROWK=k forces k (results are identical for every k) */
 static long exact_rowk(const pht_ctx *c) {
   if (const char *e = getenv("PHT_ROWK")) return std::max(0L, std::min(atol(e), c->n_exact));
+  /* by exact observations per one-lane slot (kSpreadLanes ~ the resident
+   * lanes of one MI355X); measured (tools/rowk_sweep.sh, tools/latency.py,
+   * profiles/r02/rows): the fewer per lane, the more the longest paths set
+   * the sweep time and the more rows pay (the launcher caps rows at half
+   * the resident blocks) */
+  const long L = kSpreadLanes;
+  if (c->n_exact <= L) return 4096;
+  if (c->n_exact <= 2 * L) return 2048;
+  if (c->n_exact <= 5 * L) return 128;
   return 0;
 }
 

@@ -453,6 +453,7 @@ __device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lan
   }
   const int j = st.j;
   RowDens<NT> f{id, j, y_t, P.S(j, j), id.sv ? P.W(j, id.ix) : 0.0, st.E0, 0.0, -1.0};
+  PHT_STAMP(ln, 1);
   double xsamp = 0.0;
   int ainfo = 0;
   bool fin = false;
@@ -484,6 +485,7 @@ __device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lan
       ev.y = odd ? yk : ev.y;
     }
   }
+  PHT_STAMP(ln, 2);
   /* ---- pending rows: the update ending the rejected iteration */
   if (pend && !bigm && ev.cnt + 2 > kRowCap) {
     /* hand the envelope to the general code (private copy in every lane) */
@@ -497,12 +499,13 @@ __device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lan
   }
   const bool big = pend && bigm;
   if (pend && !big) row_insert<NT>(ev, pd, f, ln, rl);
+  PHT_STAMP(ln, 3);
   const bool arm = (start && !fin) || (pend && !big);
   double cum = 0.0;
-  if (arm) {
-    row_meets(ev, rl);
-    cum = row_cumulate(ev, rl);
-  }
+  if (arm) row_meets(ev, rl);
+  PHT_STAMP(ln, 4);
+  if (arm) cum = row_cumulate(ev, rl);
+  PHT_STAMP(ln, 5);
   if (start && !fin) {
     pd.yprev = f(0.0); /* xprev = 0 lies in [xl, xr] = [0, y_t] */
     ln.neval++;
@@ -513,16 +516,24 @@ __device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lan
     ainfo = 4;
     fin = true;
   }
+  PHT_STAMP(ln, 6);
   bool acc = false;
   const bool itr = arm && !fin;
+  WPt q;
+  double yv = 0.0, ynew = 0.0;
   if (itr) {
-    WPt q;
     const double pu = dev_u(ln.r);
     row_invert(ev, cum, rl, pu, q);
     const double u = dev_u(ln.r) * q.ey;
-    const double yv = logshift(u, ev.ymax);
-    const double ynew = f(q.x);
+    yv = logshift(u, ev.ymax);
+  }
+  PHT_STAMP(ln, 7);
+  if (itr) {
+    ynew = f(q.x);
     ln.neval++;
+  }
+  PHT_STAMP(ln, 8);
+  if (itr) {
     if (yv >= ynew) {
       pd.px = q.x; pd.py = ynew; pd.pey = expshift(ynew, ev.ymax); pd.pr = q.pr;
       pd.it++;
@@ -532,6 +543,7 @@ __device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lan
       acc = true;
     }
   }
+  PHT_STAMP(ln, 9);
   /* ---- rare: envelopes beyond kRowCap, one-lane code on the private copy */
   if (big) {
     double E0f[NT];
@@ -551,10 +563,12 @@ __device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lan
       f.El = v;
     }
   }
+  PHT_STAMP(ln, 10);
   if (acc || fin) {
     pend = false;
     row_jump_finish<NT>(P, id, ln, sk, st, f, xsamp, ainfo);
   }
+  PHT_STAMP(ln, 11);
 }
 
 }  // namespace pht

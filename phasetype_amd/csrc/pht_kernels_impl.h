@@ -767,6 +767,11 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
   long pos = 0;
   bool have = false, done = false;
   unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
+#ifdef PHT_STAMPS
+  ln.st_last = __builtin_amdgcn_s_memtime();
+  for (int q = 0; q < 15; q++) ln.st_acc[q] = 0ull;
+  ln.st_rounds = 0ull;
+#endif
   for (;;) {
     bool need = false;
     if (have && !pend) pht_stream_topup(&ln.r);
@@ -819,15 +824,28 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
       need = true;
       break;
     }
+    PHT_STAMP(ln, 0);
     if (!__any(need) && !__any(pend) && !__any(!done)) break;
+#ifdef PHT_STAMPS
+    ln.st_rounds++;
+#endif
     if (need || pend) pht_stream_topup(&ln.r);
+    PHT_STAMP(ln, 12);
     row_round<NT>(P, id, ln, ev, benv, sk, st, need, pend, bigm, pd);
   }
+#ifdef PHT_STAMPS
+  (void)c_obs; (void)c_neval; (void)c_flag; (void)c_nd; (void)c_jump;
+  if ((threadIdx.x & 63) == 0) {
+    lds_add(&xc[0], ln.st_rounds);
+    for (int q = 0; q < 15; q++) lds_add(&xc[1 + q], ln.st_acc[q]);
+  }
+#else
   lds_add(&xc[0], (unsigned long long)c_obs);
   lds_add(&xc[1], (unsigned long long)c_neval);
   lds_add(&xc[2], (unsigned long long)c_flag);
   lds_add(&xc[3], (unsigned long long)c_nd);
   lds_add(&xc[4], (unsigned long long)c_jump);
+#endif
   __syncthreads();
   unsigned long long *g = a.stats;
   for (int k = threadIdx.x; k < n; k += blockDim.x) {
@@ -897,14 +915,19 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
     return e;
   /* the rowk longest observations on 16-lane rows (kBlock / kRowW per
    * block), ahead of the one-lane blocks in the same launch */
-  SweepArgs b = a;
-  b.rowk = row_ok<NT>() ? std::max(0L, std::min(a.rowk, a.count)) : 0;
-  b.rowblk = (int)((b.rowk + (kBlock / kRowW) - 1) / (kBlock / kRowW));
-  long want = (a.count - b.rowk + kBlock - 1) / kBlock;
   /* blocks per CU: the occupancy limit, or fewer (a.occ) when the shard is
    * small and the longest paths, not throughput, set the time */
   const int bpc = (a.occ > 0 && a.occ < occ) ? a.occ : occ;
-  long grid = (long)cus * bpc - b.rowblk;
+  const long slots = (long)cus * bpc;
+  SweepArgs b = a;
+  /* rows take at most half the resident blocks: the one-lane blocks (the
+   * rest of the range) must be resident too (a persistent block that
+   * started late would still own its claim chunks) */
+  const long rowmax = (slots / 2) * (kBlock / kRowW);
+  b.rowk = row_ok<NT>() ? std::max(0L, std::min(std::min(a.rowk, a.count), rowmax)) : 0;
+  b.rowblk = (int)((b.rowk + (kBlock / kRowW) - 1) / (kBlock / kRowW));
+  const long want = (a.count - b.rowk + kBlock - 1) / kBlock;
+  long grid = slots - b.rowblk;
   if (grid > want) grid = want;
   if (grid < 0) grid = 0;
   if (grid + b.rowblk < 1) return hipSuccess;

@@ -165,7 +165,8 @@ def test_grid_occupancy_invariance(gpu, monkeypatch, occ):
 
 
 @pytest.mark.parametrize("knob,value", [("PHT_CENS_SERIAL", "1"), ("PHT_HOT", "500"), ("PHT_NEWCAP", "0"),
-                                        ("PHT_SPREAD", "1"), ("PHT_FORCE_NT0", "1")])
+                                        ("PHT_SPREAD", "1"), ("PHT_FORCE_NT0", "1"), ("PHT_ROWK", "0"),
+                                        ("PHT_ROWK", "64"), ("PHT_ROWK", "100000")])
 def test_launch_knobs_invariance(gpu, monkeypatch, knob, value):
     """Launch-shape knobs (serial censored range, wave priority, no new-
     observation cap, lane-major first claims, runtime-n kernels) change no
@@ -183,6 +184,7 @@ def test_launch_knobs_invariance(gpu, monkeypatch, knob, value):
     sw.close()
     L = 2 * n + n * n
     assert np.array_equal(ref[:L], got[:L])
+    assert got[L] == len(y)  # every observation sampled
 
 
 @pytest.mark.parametrize("group", [1, 2, 4, 8])
