@@ -242,7 +242,7 @@ __device__ __forceinline__ void arms_cumulate_u(Env &e) {
 
 template <class Env>
 __device__ __forceinline__ void arms_cumulate(Env &e) {
-  if (e.cnt <= kArmsU) {
+  if (Env::kUnroll && e.cnt <= kArmsU) {
     arms_cumulate_u(e);
     return;
   }
@@ -288,7 +288,7 @@ __device__ __forceinline__ void arms_invert(Env &e, double prob, WPt &p) {
   int q = e.cnt - 1;
   const double u = prob * e.CUM(q);
   double cl, cr;
-  if (e.cnt <= kArmsU) {
+  if (Env::kUnroll && e.cnt <= kArmsU) {
     /* q moves down from last while cum[q-1] > u (scan unrolled) */
     const int last = e.cnt - 1;
     double cs[kArmsU];
@@ -341,7 +341,7 @@ template <class Env, class F>
 __device__ __forceinline__ void arms_update(Env &e, const WPt &p, F &f, Lane &ln) {
   if (e.cnt > kArmsNPoint - 2) return;
   const int pr = p.pr;
-  if (e.cnt <= kArmsU) {
+  if (Env::kUnroll && e.cnt <= kArmsU) {
     /* positions pr..cnt-1 move up by 2: read all, write positions 2..kArmsU+1 */
     const int last = e.cnt - 1;
     double xs[kArmsU + 2], ys[kArmsU + 2];

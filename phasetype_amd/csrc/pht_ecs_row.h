@@ -108,6 +108,7 @@ struct RowObs {
   double yt;
   int j, njump;
   bool haveE0, haveDen;
+  bool fold; /* the absorb test after a jump runs at the start of the next round (row_round) */
   double den;
   double E0; /* e^{lambda_slot yt} */
 };
@@ -231,8 +232,9 @@ __device__ __forceinline__ RowMax rowmax_step(RowMax m) {
 }
 
 /* round_cumulate on the row: ymax, then this lane's area (segment rl-1 ->
- * rl) and the prefix sum in position order; returns cum at position rl */
-__device__ __forceinline__ double row_cumulate(RowEnv &e, int rl) {
+ * rl) and the prefix sum in position order; returns cum at position rl
+ * (and ey = expshift(y, ymax) there, which invert reuses) */
+__device__ __forceinline__ double row_cumulate(RowEnv &e, int rl, double &ey) {
   RowMax m;
   m.v = e.y;
   m.k = (rl < e.cnt) ? rl : 64 + rl;
@@ -243,6 +245,7 @@ __device__ __forceinline__ double row_cumulate(RowEnv &e, int rl) {
   const double ymax = m.v;
   e.ymax = ymax;
   const double eyk = expshift(e.y, ymax);
+  ey = eyk;
   const double xp = dpp_d<dpp_shr(1)>(e.x), yp = dpp_d<dpp_shr(1)>(e.y), eyp = dpp_d<dpp_shr(1)>(eyk);
   const double xk = e.x, yk = e.y;
   const double lin = 0.5 * (eyk + eyp) * (xk - xp);
@@ -259,8 +262,10 @@ __device__ __forceinline__ double row_cumulate(RowEnv &e, int rl) {
   return cum;
 }
 
-/* round_invert on the row (cum: this lane's cumulative area) */
-__device__ __forceinline__ void row_invert(const RowEnv &e, double cum, int rl, double prob, WPt &p) {
+/* round_invert on the row (cum, ey: this lane's cumulative area and
+ * expshift(y, ymax) from row_cumulate; the same values round_invert
+ * recomputes) */
+__device__ __forceinline__ void row_invert(const RowEnv &e, double cum, double ey, int rl, double prob, WPt &p) {
   const int last = e.cnt - 1;
   const double clast = row_get(cum, last);
   const double u = prob * clast;
@@ -271,13 +276,12 @@ __device__ __forceinline__ void row_invert(const RowEnv &e, double cum, int rl, 
   const double cr = row_get(cum, q), cl = row_get(cum, q - 1);
   const double xl = row_get(e.x, q - 1), xr = row_get(e.x, q);
   const double yr = row_get(e.y, q), yl = row_get(e.y, q - 1);
+  const double eyr = row_get(ey, q), eyl = row_get(ey, q - 1);
   const double prop = PHT_DIV((u - cl), (cr - cl));
-  const double eyr = expshift(yr, e.ymax);
   if (xl == xr) {
     p.x = xr; p.y = yr; p.ey = eyr;
     return;
   }
-  const double eyl = expshift(yl, e.ymax);
   if (fabs(yr - yl) < kYEps) {
     if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
       p.x = xl + (PHT_DIV((xr - xl), (eyr - eyl))) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
@@ -425,6 +429,7 @@ __device__ __forceinline__ void row_jump_finish(const Par<NT> &P, const RowId &i
     for (int q = 0; q < NT; q++) dsel = (q == sel) ? accs[q] : dsel;
     st.den = dsel;
     st.haveDen = (cnt > 0);
+    st.fold = st.haveDen;
   }
   if (id.lead) {
     sk.z(j, d);
@@ -442,7 +447,7 @@ __device__ __forceinline__ void row_jump_finish(const Par<NT> &P, const RowId &i
  * runs it, replicated).
  */
 template <int NT, class Sink>
-__device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lane &ln, RowEnv &ev, EnvPrivate &benv,
+__device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId &id, Lane &ln, RowEnv &ev, EnvPrivateBig &benv,
                                           Sink &sk, RowObs &st, bool start, bool &pend, bool &bigm, ArmsPend &pd) {
   const int rl = id.rl;
   const double y_t = st.yt;
@@ -457,30 +462,51 @@ __device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lan
   double xsamp = 0.0;
   int ainfo = 0;
   bool fin = false;
-  /* ---- starting rows: initial envelope (4 evaluations side by side) */
+  /* ---- starting rows: initial envelope (4 evaluations side by side).
+   * A path that has just jumped (st.fold) first takes its absorb test
+   * (ecs_try_absorb: same draw, same arithmetic); it is computed alongside
+   * the envelope, which is dropped when the path ends here. */
   if (start) {
+    const bool test = st.fold;
+    st.fold = false;
+    const bool capj = test && st.njump >= kMaxJumps;
+    const bool draw = test && !capj && P.s(j) > 0.0;
+    double U = 1.0;
+    if (draw) U = dev_u(ln.r);
+    const double pab = pht_exp(fma(P.S(j, j), y_t, P.logs(j)) - pht_log(st.den));
     double xinit[4];
     xinit[0] = (y_t) / 1e6;
     xinit[1] = (y_t) / 3.0;
     xinit[2] = xinit[1] * 2.0;
     xinit[3] = y_t - xinit[0];
-    if ((xinit[0] <= 0.0) || (xinit[3] >= y_t)) {
+    const bool e1003 = (xinit[0] <= 0.0) || (xinit[3] >= y_t);
+    const bool e1004 = !e1003 && (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]);
+    double acc[4];
+    f.init4(xinit, acc);
+    /* lanes 1, 3, 5, 7: the starting points; 0 and 8: the interval ends */
+    const int k = (rl >> 1) & 3;
+    const double xk = (k == 0) ? xinit[0] : (k == 1) ? xinit[1] : (k == 2) ? xinit[2] : xinit[3];
+    const double ak = (k == 0) ? acc[0] : (k == 1) ? acc[1] : (k == 2) ? acc[2] : acc[3];
+    const double yk = pht_log(ak) + f.Sjj * xk;
+    if (capj || (draw && U < pab)) { /* the path is complete */
+      if (capj) ln.flags |= kFlagJumpCap;
+      if (id.lead) {
+        sk.N(j, j);
+        sk.z(j, y_t);
+        sk.pre(j);
+      }
+      return true;
+    }
+    if (e1003) {
       ainfo = 1003;
       fin = true;
-    } else if (xinit[1] <= xinit[0] || xinit[2] <= xinit[1] || xinit[3] <= xinit[2]) {
+    } else if (e1004) {
       ainfo = 1004;
       fin = true;
     } else {
-      double acc[4];
-      f.init4(xinit, acc);
       ln.neval += 4;
       ev.cnt = 9;
-      /* lanes 1, 3, 5, 7: the starting points; 0 and 8: the interval ends */
-      const int k = (rl >> 1) & 3;
-      const double xk = (k == 0) ? xinit[0] : (k == 1) ? xinit[1] : (k == 2) ? xinit[2] : xinit[3];
-      const double ak = (k == 0) ? acc[0] : (k == 1) ? acc[1] : (k == 2) ? acc[2] : acc[3];
       const bool odd = (rl & 1) && rl < 8;
-      const double yk = pht_log(ak) + f.Sjj * xk;
       ev.x = (rl == 0) ? 0.0 : (odd ? xk : ((rl == 8) ? y_t : ev.x));
       ev.y = odd ? yk : ev.y;
     }
@@ -501,10 +527,10 @@ __device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lan
   if (pend && !big) row_insert<NT>(ev, pd, f, ln, rl);
   PHT_STAMP(ln, 3);
   const bool arm = (start && !fin) || (pend && !big);
-  double cum = 0.0;
+  double cum = 0.0, eyv = 0.0;
   if (arm) row_meets(ev, rl);
   PHT_STAMP(ln, 4);
-  if (arm) cum = row_cumulate(ev, rl);
+  if (arm) cum = row_cumulate(ev, rl, eyv);
   PHT_STAMP(ln, 5);
   if (start && !fin) {
     pd.yprev = f(0.0); /* xprev = 0 lies in [xl, xr] = [0, y_t] */
@@ -523,7 +549,7 @@ __device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lan
   double yv = 0.0, ynew = 0.0;
   if (itr) {
     const double pu = dev_u(ln.r);
-    row_invert(ev, cum, rl, pu, q);
+    row_invert(ev, cum, eyv, rl, pu, q);
     const double u = dev_u(ln.r) * q.ey;
     yv = logshift(u, ev.ymax);
   }
@@ -569,6 +595,7 @@ __device__ __forceinline__ void row_round(const Par<NT> &P, const RowId &id, Lan
     row_jump_finish<NT>(P, id, ln, sk, st, f, xsamp, ainfo);
   }
   PHT_STAMP(ln, 11);
+  return false;
 }
 
 }  // namespace pht

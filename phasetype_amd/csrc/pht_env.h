@@ -26,6 +26,7 @@
 namespace pht {
 
 struct EnvPrivate {
+  static constexpr bool kUnroll = true; /* arms_*: unrolled code for envelopes of <= kArmsU points */
   double x[100], y[100], cum[100];
   int cnt;
   double ymax;
@@ -35,6 +36,13 @@ struct EnvPrivate {
   __device__ __forceinline__ void sX(int k, double v) { x[k] = v; }
   __device__ __forceinline__ void sY(int k, double v) { y[k] = v; }
   __device__ __forceinline__ void sCUM(int k, double v) { cum[k] = v; }
+};
+
+/* EnvPrivate for envelopes known to exceed kArmsU points (the ECS row
+ * kernel's general-code continuation): the rolled loops only, which keeps
+ * the unrolled code's register arrays out of the caller (same values) */
+struct EnvPrivateBig : EnvPrivate {
+  static constexpr bool kUnroll = false;
 };
 
 #ifndef PHT_PRIV
@@ -48,6 +56,7 @@ struct EnvPrivate {
  * rejection chains) uses the full accessors. */
 template <int K, int STRIDE>
 struct EnvLdsXY {
+  static constexpr bool kUnroll = true;
   static constexpr int kSpill = 100 - K;
   PHT_LDS double *l;   /* lane's element 0 */
   PHT_PRIV double *ov; /* [2][kSpill] x, y beyond K */

@@ -34,8 +34,11 @@ struct SweepArgs {
   int newcap;                  /* ECS exact: observations a lane may start per round (0 = no limit) */
   double hoty;                 /* ECS exact: waves with a path whose remaining time exceeds hoty issue at high priority (0 = off) */
   int allcens;                 /* ECS: every observation of the launch is right-censored (jump-converged kernel) */
-  long rowk;                   /* ECS exact: positions [0, rowk) (the longest paths) run one per 16-lane row */
-  int rowblk;                  /* ECS exact: blocks of the launch serving those rows (set by the launcher) */
+  long rowk;                   /* ECS exact: the first rowk positions (the longest paths) run one per 16-lane row;
+                                  in the kernel: the rowk positions before begin */
+  int rowblk;                  /* ECS exact: blocks of the launch serving those rows, before the nmain one-lane
+                                  blocks (both set by the launcher) */
+  int nmain;
   int rowprio;                 /* ECS exact: wave priority of the row blocks (s_setprio 0-3) */
   /* MHRS attempt search (pht_kernels.hip, MHRS section): per chain task
    * (position * (1 + mhit) + c) its first success (attempt << 8 | pre), two

@@ -709,7 +709,7 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
 
 /*
  * The longest exact observations, one per 16-lane row (pht_ecs_row.h):
- * positions [0, a.rowk) of the launch range (decreasing y), block b of the
+ * the a.rowk positions before the one-lane range (decreasing y), block b of the
  * nblk row blocks taking positions b, b + nblk, ... through its LDS cursor.
  * The row waves issue at raised priority: they carry the sweep's critical
  * path while one-lane blocks share their CUs.
@@ -758,15 +758,32 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
   Lane ln;
   RowObs st;
-  st.yt = 0.0; st.j = 0; st.njump = 0; st.haveE0 = false; st.haveDen = false; st.den = 0.0; st.E0 = 0.0;
+  st.yt = 0.0; st.j = 0; st.njump = 0; st.haveE0 = false; st.haveDen = false; st.fold = false; st.den = 0.0;
+  st.E0 = 0.0;
   RowEnv ev;
   ev.x = 0.0; ev.y = 0.0; ev.cnt = 0; ev.ymax = 0.0;
-  EnvPrivate benv;
+  EnvPrivateBig benv;
   ArmsPend pd;
   bool pend = false, bigm = false;
   long pos = 0;
   bool have = false, done = false;
   unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
+  /* the path of the row is complete (its statistics recorded) */
+  auto complete = [&]() {
+    const uint32_t nd = pht_stream_pos(&ln.r);
+    if (id.lead) {
+      if (DEBUG) {
+        a.dbg_flags[pos] = ln.flags;
+        a.dbg_ndraw[pos] = nd;
+      }
+      c_obs++;
+      c_neval += ln.neval;
+      c_flag += ln.flags ? 1u : 0u;
+      c_nd += nd;
+      c_jump += ln.njump;
+    }
+    have = false;
+  };
 #ifdef PHT_STAMPS
   ln.st_last = __builtin_amdgcn_s_memtime();
   for (int q = 0; q < 15; q++) ln.st_acc[q] = 0ull;
@@ -785,7 +802,7 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
           done = true;
           break;
         }
-        pos = a.begin + p;
+        pos = a.begin - a.rowk + p; /* the rows' positions precede the launch range */
         pht_stream_init(&ln.r, a.k0, a.k1, a.gid[pos], 0u, a.sweep);
         ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
         if (DEBUG) {
@@ -803,22 +820,12 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
         st.njump = 0;
         st.haveE0 = false;
         st.haveDen = false;
+        st.fold = false;
         have = true;
       }
-      if (row_try_absorb<NT>(P, id, ln, sk, st)) {
-        const uint32_t nd = pht_stream_pos(&ln.r);
-        if (id.lead) {
-          if (DEBUG) {
-            a.dbg_flags[pos] = ln.flags;
-            a.dbg_ndraw[pos] = nd;
-          }
-          c_obs++;
-          c_neval += ln.neval;
-          c_flag += ln.flags ? 1u : 0u;
-          c_nd += nd;
-          c_jump += ln.njump;
-        }
-        have = false;
+      /* after a jump the absorb test runs inside the round (row_round) */
+      if (!st.fold && row_try_absorb<NT>(P, id, ln, sk, st)) {
+        complete();
         continue;
       }
       need = true;
@@ -831,7 +838,7 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
 #endif
     if (need || pend) pht_stream_topup(&ln.r);
     PHT_STAMP(ln, 12);
-    row_round<NT>(P, id, ln, ev, benv, sk, st, need, pend, bigm, pd);
+    if (row_round<NT>(P, id, ln, ev, benv, sk, st, need, pend, bigm, pd)) complete();
   }
 #ifdef PHT_STAMPS
   (void)c_obs; (void)c_neval; (void)c_flag; (void)c_nd; (void)c_jump;
@@ -858,33 +865,39 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
     if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
 }
 
-/* waves per SIMD the ECS kernel is compiled for: two at n = 15, where the
+/* waves per SIMD the ECS kernel is compiled for (its DEBUG instantiation,
+ * per-observation outputs for the parity tests, is left unconstrained): two
+ * at n = 10 with row blocks (the row code would otherwise take it to one)
+ * and at n = 15, where the
  * W row read from LDS (EcsDens) lets it fit (255 VGPRs, no spills, per the
  * built library's metadata: tools/kernel_regs.py); otherwise what the
  * registers allow (PHT_ECS_WAVES=k forces every n).  The DEBUG=true
  * instantiations (per-observation outputs for the parity tests) may spill a
  * few VGPRs: they are never timed. */
-template <int NT>
+template <int NT, bool ROWS = false>
 constexpr int ecs_waves() {
-  return PHT_ECS_WAVES > 0 ? PHT_ECS_WAVES : (NT == 15 ? 2 : 1);
+  return PHT_ECS_WAVES > 0 ? PHT_ECS_WAVES : ((NT == 15 || (ROWS && NT == 10)) ? 2 : 1);
 }
-template <int NT, bool DEBUG>
+template <int NT, bool DEBUG, bool ROWS>
 __global__ void __launch_bounds__(kBlock)
-__attribute__((amdgpu_waves_per_eu(ecs_waves<NT>())))
+__attribute__((amdgpu_waves_per_eu(DEBUG ? 1 : ecs_waves<NT, ROWS>())))
 ecs_exact_kernel(SweepArgs a) {
-  unsigned blk = blockIdx.x, nblk = gridDim.x;
-  if constexpr (row_ok<NT>()) {
-    /* blocks [0, rowblk): the a.rowk longest observations, one per row */
-    if (blk < (unsigned)a.rowblk) {
-      ecs_row_body<NT, DEBUG>(a, blk, (unsigned)a.rowblk);
+  if constexpr (ROWS) {
+    /* blocks [0, rowblk): the a.rowk longest observations, one per row
+     * (positions [begin - rowk, begin)), dispatched first so that a kernel
+     * running concurrently (the censored range) cannot take their slots;
+     * then the nmain one-lane blocks over the launch range (set by the
+     * launcher).  A separate instantiation: without rows the kernel is the
+     * one-lane body alone (its register and SGPR allocation untouched by the
+     * row code) */
+    if (__builtin_expect(blockIdx.x < (unsigned)a.rowblk, 0)) {
+      ecs_row_body<NT, DEBUG>(a, blockIdx.x, (unsigned)a.rowblk);
       return;
     }
-    blk -= (unsigned)a.rowblk;
-    nblk -= (unsigned)a.rowblk;
-    a.begin += a.rowk;
-    a.count -= a.rowk;
+    ecs_exact_body<NT, DEBUG>(a, blockIdx.x - (unsigned)a.rowblk, (unsigned)a.nmain);
+  } else {
+    ecs_exact_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
   }
-  ecs_exact_body<NT, DEBUG>(a, blk, nblk);
 }
 
 /*
@@ -908,11 +921,13 @@ static int smem_bytes_ecs(int n) {
 
 template <int NT, bool DEBUG>
 static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
-  static LaunchCfg cfg;
+  static LaunchCfg cfg, cfgr;
   const int sm = smem_bytes_ecs(a.n);
+  const bool rows = row_ok<NT>() && a.rowk > 0;
+  const void *kfn = rows ? (const void *)ecs_exact_kernel<NT, DEBUG, row_ok<NT>()>
+                         : (const void *)ecs_exact_kernel<NT, DEBUG, false>;
   int occ = 0, cus = 0;
-  if (hipError_t e = launch_config(cfg, (const void *)ecs_exact_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
-    return e;
+  if (hipError_t e = launch_config(rows ? cfgr : cfg, kfn, sm, &occ, &cus); e != hipSuccess) return e;
   /* the rowk longest observations on 16-lane rows (kBlock / kRowW per
    * block), ahead of the one-lane blocks in the same launch */
   /* blocks per CU: the occupancy limit, or fewer (a.occ) when the shard is
@@ -926,12 +941,19 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
   const long rowmax = (slots / 2) * (kBlock / kRowW);
   b.rowk = row_ok<NT>() ? std::max(0L, std::min(std::min(a.rowk, a.count), rowmax)) : 0;
   b.rowblk = (int)((b.rowk + (kBlock / kRowW) - 1) / (kBlock / kRowW));
-  const long want = (a.count - b.rowk + kBlock - 1) / kBlock;
+  b.begin = a.begin + b.rowk;
+  b.count = a.count - b.rowk;
+  const long want = (b.count + kBlock - 1) / kBlock;
   long grid = slots - b.rowblk;
   if (grid > want) grid = want;
   if (grid < 0) grid = 0;
+  b.nmain = (int)grid;
   if (grid + b.rowblk < 1) return hipSuccess;
-  hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG>), dim3((unsigned)(grid + b.rowblk)), dim3(kBlock), sm, st, b);
+  if (rows)
+    hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG, row_ok<NT>()>), dim3((unsigned)(grid + b.rowblk)), dim3(kBlock), sm,
+                       st, b);
+  else
+    hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG, false>), dim3((unsigned)grid), dim3(kBlock), sm, st, b);
   return hipGetLastError();
 }
 

@@ -25,7 +25,8 @@ def regs(lib):
 
 
 @pytest.mark.parametrize("nt", [3, 5, 10, 15])
-@pytest.mark.parametrize("kind", ["ecs_exact_kernelILi{nt}ELb0E", "ecs_chains_kernelILi{nt}EE"])
+@pytest.mark.parametrize("kind", ["ecs_exact_kernelILi{nt}ELb0ELb0E", "ecs_exact_kernelILi{nt}ELb0ELb1E",
+                                  "ecs_chains_kernelILi{nt}EE"])
 def test_ecs_two_waves_no_spill(regs, nt, kind):
     key = kind.format(nt=nt)
     hits = {k: v for k, v in regs.items() if key in k}
@@ -47,7 +48,7 @@ def test_ecs_debug_instantiations(regs, nt):
     """Informational bound on the DEBUG=true ECS kernels (per-observation
     outputs; the parity tests run them, nothing times them): they may spill
     a few VGPRs (n = 15: 6, n = 20: 18 at r01) but must not blow up."""
-    key = f"ecs_exact_kernelILi{nt}ELb1E"
+    key = f"ecs_exact_kernelILi{nt}ELb1ELb{int(0 < nt <= 16)}E"
     hits = {k: v for k, v in regs.items() if key in k}
     assert len(hits) == 1, (key, list(hits))
     (name, d), = hits.items()
