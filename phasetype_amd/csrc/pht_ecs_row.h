@@ -53,6 +53,21 @@ constexpr int kDppHalfMirror = 0x141; /* lane l <- lane 7 - l (in each half row)
 constexpr int dpp_shl(int s) { return 0x100 + s; } /* lane l <- lane l + s */
 constexpr int dpp_shr(int s) { return 0x110 + s; } /* lane l <- lane l - s */
 
+/* A cross-lane read must run where the whole row is active: DPP and
+ * ds_bpermute read a source lane's register whether or not that lane took
+ * part, so a read the compiler sank into a lane-divergent branch would see
+ * stale values (it did: a select turned into a branch around the row
+ * scan's shifts).  pin() materialises a value at its program point (an
+ * empty volatile asm: not sunk, not reordered past other volatile asm);
+ * dpp_pd pins the shifts whose values are used only under lane-divergent
+ * conditions (the reductions and row_get feed unconditional arithmetic or
+ * row-uniform branches, and stay unpinned so their chains interleave). */
+template <class T>
+__device__ __forceinline__ T pin(T v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 /* out-of-row sources read 0 (bound_ctrl off, old = 0); every caller selects
  * such lanes away */
 template <int CTRL>
@@ -65,6 +80,11 @@ __device__ __forceinline__ double dpp_d(double v) {
   const unsigned lo = (unsigned)dpp_i<CTRL>((int)(unsigned)u);
   const unsigned hi = (unsigned)dpp_i<CTRL>((int)(unsigned)(u >> 32));
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+/* a row shift whose value is used only under lane-divergent conditions */
+template <int CTRL>
+__device__ __forceinline__ double dpp_pd(double v) {
+  return pin(dpp_d<CTRL>(v));
 }
 
 /* value of lane k of the row (k row-uniform) */
@@ -166,12 +186,12 @@ __device__ __forceinline__ void row_meets(RowEnv &e, int rl) {
   const int last = e.cnt - 1;
   const int K = rl;
   /* slope of the segment from this (odd) point to the next odd point */
-  const double xb = dpp_d<dpp_shl(2)>(e.x), yb = dpp_d<dpp_shl(2)>(e.y);
+  const double xb = dpp_pd<dpp_shl(2)>(e.x), yb = dpp_pd<dpp_shl(2)>(e.y);
   const double q = PHT_DIV((yb - e.y), (xb - e.x));
   const double sb = (e.y == yb && q == 0.0) ? ((e.x - xb < 0.0) ? -0.0 : 0.0) : q;
-  const double glv = dpp_d<dpp_shr(3)>(q), grlv = dpp_d<dpp_shr(1)>(q), grv = dpp_d<dpp_shl(1)>(sb);
-  const double xm1 = dpp_d<dpp_shr(1)>(e.x), ym1 = dpp_d<dpp_shr(1)>(e.y);
-  const double xp1 = dpp_d<dpp_shl(1)>(e.x), yp1 = dpp_d<dpp_shl(1)>(e.y);
+  const double glv = dpp_pd<dpp_shr(3)>(q), grlv = dpp_pd<dpp_shr(1)>(q), grv = dpp_pd<dpp_shl(1)>(sb);
+  const double xm1 = dpp_pd<dpp_shr(1)>(e.x), ym1 = dpp_pd<dpp_shr(1)>(e.y);
+  const double xp1 = dpp_pd<dpp_shl(1)>(e.x), yp1 = dpp_pd<dpp_shl(1)>(e.y);
   const bool il = (K >= 3), ir = (K + 3 <= last), irl = (K >= 1 && K + 1 <= last);
   const double xk = e.x, yk = e.y;
   double gl = il ? glv : 0.0, gr = ir ? grv : 0.0, grl = irl ? grlv : 0.0, dl = 0.0, dr = 0.0;
@@ -235,30 +255,59 @@ __device__ __forceinline__ RowMax rowmax_step(RowMax m) {
  * rl) and the prefix sum in position order; returns cum at position rl
  * (and ey = expshift(y, ymax) there, which invert reuses) */
 __device__ __forceinline__ double row_cumulate(RowEnv &e, int rl, double &ey) {
-  RowMax m;
-  m.v = e.y;
-  m.k = (rl < e.cnt) ? rl : 64 + rl;
-  m = rowmax_step<kDppMirror>(m);
-  m = rowmax_step<kDppHalfMirror>(m);
-  m = rowmax_step<kDppQuadRev>(m);
-  m = rowmax_step<kDppQuadX1>(m);
-  const double ymax = m.v;
+  /* fmax reduction (NaN ignored, as the scan ignores NaN at positions >=
+   * 1); it can differ from the scan only for a NaN at position 0 or a zero
+   * maximum (+0 against -0): those rows take the exact order reduction */
+  double mx = (rl < e.cnt) ? e.y : -INFINITY;
+  mx = fmax(mx, dpp_d<kDppMirror>(mx));
+  mx = fmax(mx, dpp_d<kDppHalfMirror>(mx));
+  mx = fmax(mx, dpp_d<kDppQuadRev>(mx));
+  mx = fmax(mx, dpp_d<kDppQuadX1>(mx));
+  const bool nan0 = row_ballot(rl == 0 && e.y != e.y) != 0u;
+  if (nan0 || mx == 0.0) {
+    RowMax m;
+    m.v = e.y;
+    m.k = (rl < e.cnt) ? rl : 64 + rl;
+    m = rowmax_step<kDppMirror>(m);
+    m = rowmax_step<kDppHalfMirror>(m);
+    m = rowmax_step<kDppQuadRev>(m);
+    m = rowmax_step<kDppQuadX1>(m);
+    mx = m.v;
+  }
+  const double ymax = mx;
   e.ymax = ymax;
   const double eyk = expshift(e.y, ymax);
   ey = eyk;
-  const double xp = dpp_d<dpp_shr(1)>(e.x), yp = dpp_d<dpp_shr(1)>(e.y), eyp = dpp_d<dpp_shr(1)>(eyk);
+  const double xp = dpp_pd<dpp_shr(1)>(e.x), yp = dpp_pd<dpp_shr(1)>(e.y), eyp = dpp_pd<dpp_shr(1)>(eyk);
   const double xk = e.x, yk = e.y;
   const double lin = 0.5 * (eyk + eyp) * (xk - xp);
   const double ex = (PHT_DIV((eyk - eyp), (yk - yp))) * (xk - xp);
   const double a = (xp == xk) ? 0. : ((fabs(yk - yp) < kYEps) ? lin : ex);
-  /* cum_k = cum_{k-1} + a_k, k = 1 .. cnt-1, in order (one step per point) */
+  /* cum_k = (((0 + a_1) + a_2) + ...) + a_k in this order: lane k takes
+   * a_{k-s} by one row shift per s (independent moves, issued together) and
+   * adds them from s = k - 1 down to 0; the dependent chain is the adds */
   double cum = 0.;
+#ifdef PHT_ROW_OLDSCAN
 #pragma unroll
   for (int t = 1; t < kRowCap; t++) {
     if (!__any(t < e.cnt)) break;
     const double v = dpp_d<dpp_shr(1)>(cum);
     cum = (rl == t) ? v + a : cum;
   }
+  return cum;
+#endif
+  /* (an invalid step adds +0 to cum = +0: cum is never -0, so the sum is
+   * the select's value) */
+#define PHT_ROW_CUM(S)                           \
+  {                                              \
+    const double t_ = dpp_pd<dpp_shr(S)>(a);     \
+    cum = cum + ((rl - (S) >= 1) ? t_ : 0.0);    \
+  }
+  PHT_ROW_CUM(14); PHT_ROW_CUM(13); PHT_ROW_CUM(12); PHT_ROW_CUM(11); PHT_ROW_CUM(10);
+  PHT_ROW_CUM(9); PHT_ROW_CUM(8); PHT_ROW_CUM(7); PHT_ROW_CUM(6); PHT_ROW_CUM(5);
+  PHT_ROW_CUM(4); PHT_ROW_CUM(3); PHT_ROW_CUM(2); PHT_ROW_CUM(1);
+#undef PHT_ROW_CUM
+  cum = (rl >= 1) ? cum + a : cum;
   return cum;
 }
 
@@ -300,7 +349,7 @@ __device__ __forceinline__ void row_invert(const RowEnv &e, double cum, double e
 template <int NT>
 __device__ __forceinline__ void row_insert(RowEnv &e, const ArmsPend &pd, RowDens<NT> &f, Lane &ln, int rl) {
   const int pr = pd.pr, last = e.cnt - 1;
-  const double xs = dpp_d<dpp_shr(2)>(e.x), ys = dpp_d<dpp_shr(2)>(e.y);
+  const double xs = dpp_pd<dpp_shr(2)>(e.x), ys = dpp_pd<dpp_shr(2)>(e.y);
   const bool mv = (rl >= 2) && (rl - 2 >= pr) && (rl - 2 <= last);
   e.x = mv ? xs : e.x;
   e.y = mv ? ys : e.y;
@@ -328,17 +377,30 @@ __device__ __forceinline__ void row_insert(RowEnv &e, const ArmsPend &pd, RowDen
   }
 }
 
-/* round_metropolis on the row */
-__device__ __forceinline__ double row_metropolis(const RowEnv &e, int rl, const WPt &p, double ynew, double xprev,
-                                                 double yprev, Lane &ln) {
+/* the envelope segment round_metropolis reads (xprev's): ql with
+ * X(ql) <= xprev < X(ql + 1) scanning from 0, and its two points; read as
+ * soon as the round's envelope is final (after the meets) */
+struct RowMetroSeg {
+  double xql, yql, xqr, yqr;
+};
+__device__ __forceinline__ RowMetroSeg row_metro_seg(const RowEnv &e, int rl, double xprev) {
   /* ql: while (X(ql + 1) < xprev) ql++ */
   const unsigned stop = row_ballot(rl >= 1 && !(e.x < xprev));
   const int ql = stop ? __builtin_ctz(stop) - 1 : kRowW - 2;
   const int qr = ql + 1;
-  const double xql = row_get(e.x, ql), yql = row_get(e.y, ql);
-  const double xqr = row_get(e.x, qr), yqr = row_get(e.y, qr);
-  double w = PHT_DIV((xprev - xql), (xqr - xql));
-  double zold = yql + w * (yqr - yql);
+  RowMetroSeg m;
+  m.xql = row_get(e.x, ql);
+  m.yql = row_get(e.y, ql);
+  m.xqr = row_get(e.x, qr);
+  m.yqr = row_get(e.y, qr);
+  return m;
+}
+
+/* round_metropolis on the row */
+__device__ __forceinline__ double row_metropolis(const RowMetroSeg &m, const WPt &p, double ynew, double xprev,
+                                                 double yprev, Lane &ln) {
+  double w = PHT_DIV((xprev - m.xql), (m.xqr - m.xql));
+  double zold = m.yql + w * (m.yqr - m.yql);
   double znew = p.y;
   if (yprev < zold) zold = yprev;
   if (ynew < znew) znew = ynew;
@@ -377,10 +439,33 @@ __device__ __forceinline__ bool row_try_absorb(const Par<NT> &P, const RowId &id
   return fin;
 }
 
+/* the first kRowSuccPre successors of state j (moveMass' candidates), read
+ * at the start of the round so the loads are off the finish's chain */
+constexpr int kRowSuccPre = 2;
+struct RowSucc {
+  int cnt;
+  int k[kRowSuccPre];
+  double p[kRowSuccPre], qq[kRowSuccPre]; /* P[j,k], QQs[k, slot] */
+};
+template <int NT>
+__device__ __forceinline__ RowSucc row_succ(const Par<NT> &P, const RowId &id, int j) {
+  RowSucc r;
+  r.cnt = P.nsuccP(j);
+#pragma unroll
+  for (int q = 0; q < kRowSuccPre; q++) {
+    const int k = P.succP(j, (q < NT) ? q : 0);
+    r.k[q] = k;
+    const int kc = (q < r.cnt) ? k : 0; /* entries beyond cnt are not read */
+    r.p[q] = P.P(j, kc);
+    r.qq[q] = P.QQs(kc, id.ix);
+  }
+  return r;
+}
+
 /* ecs_jump_finish: moveMass + categorical + statistics */
 template <int NT, class Sink>
 __device__ __forceinline__ void row_jump_finish(const Par<NT> &P, const RowId &id, Lane &ln, Sink &sk, RowObs &st,
-                                                const RowDens<NT> &f, double xsamp, int ainfo) {
+                                                const RowDens<NT> &f, double xsamp, int ainfo, const RowSucc &su) {
   const int j = st.j;
   const double y_t = st.yt;
   if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
@@ -395,15 +480,17 @@ __device__ __forceinline__ void row_jump_finish(const Par<NT> &P, const RowId &i
   }
   st.yt = x;
   st.haveE0 = true;
-  const int cnt = P.nsuccP(j);
+  const int cnt = su.cnt;
   double w[NT], accs[NT];
   double sum = 0.0;
 #pragma unroll
   for (int q = 0; q < NT; q++) {
     if (q < cnt) {
-      const int k = P.succP(j, q);
-      accs[q] = row_sum16(id.sv ? P.QQs(k, id.ix) * st.E0 : 0.0, id.slot, NT);
-      w[q] = P.P(j, k) * accs[q];
+      const int k = (q < kRowSuccPre) ? su.k[q] : P.succP(j, q);
+      const double qq = (q < kRowSuccPre) ? su.qq[q] : P.QQs(k, id.ix);
+      const double pjk = (q < kRowSuccPre) ? su.p[q] : P.P(j, k);
+      accs[q] = row_sum16(id.sv ? qq * st.E0 : 0.0, id.slot, NT);
+      w[q] = pjk * accs[q];
       sum += w[q];
     }
   }
@@ -423,7 +510,7 @@ __device__ __forceinline__ void row_jump_finish(const Par<NT> &P, const RowId &i
       ln.flags |= kFlagScanEnd;
       sel = cnt - 1;
     }
-    nj = (cnt > 0) ? P.succP(j, sel) : 0;
+    nj = (cnt > 0) ? ((sel < kRowSuccPre) ? su.k[sel < kRowSuccPre ? sel : 0] : P.succP(j, sel)) : 0;
     double dsel = 0.0;
 #pragma unroll
     for (int q = 0; q < NT; q++) dsel = (q == sel) ? accs[q] : dsel;
@@ -457,6 +544,7 @@ __device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId &id, Lan
     st.haveDen = false;
   }
   const int j = st.j;
+  const RowSucc su = row_succ<NT>(P, id, j);
   RowDens<NT> f{id, j, y_t, P.S(j, j), id.sv ? P.W(j, id.ix) : 0.0, st.E0, 0.0, -1.0};
   PHT_STAMP(ln, 1);
   double xsamp = 0.0;
@@ -528,7 +616,13 @@ __device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId &id, Lan
   PHT_STAMP(ln, 3);
   const bool arm = (start && !fin) || (pend && !big);
   double cum = 0.0, eyv = 0.0;
-  if (arm) row_meets(ev, rl);
+  RowMetroSeg mseg{0.0, 0.0, 0.0, 0.0};
+  if (arm) {
+    row_meets(ev, rl);
+#ifndef PHT_ROW_OLDMETRO
+    mseg = row_metro_seg(ev, rl, 0.0);
+#endif
+  }
   PHT_STAMP(ln, 4);
   if (arm) cum = row_cumulate(ev, rl, eyv);
   PHT_STAMP(ln, 5);
@@ -565,7 +659,10 @@ __device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId &id, Lan
       pd.it++;
       pend = true;
     } else {
-      xsamp = row_metropolis(ev, rl, q, ynew, 0.0, pd.yprev, ln);
+#ifdef PHT_ROW_OLDMETRO
+      mseg = row_metro_seg(ev, rl, 0.0);
+#endif
+      xsamp = row_metropolis(mseg, q, ynew, 0.0, pd.yprev, ln);
       acc = true;
     }
   }
@@ -592,7 +689,7 @@ __device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId &id, Lan
   PHT_STAMP(ln, 10);
   if (acc || fin) {
     pend = false;
-    row_jump_finish<NT>(P, id, ln, sk, st, f, xsamp, ainfo);
+    row_jump_finish<NT>(P, id, ln, sk, st, f, xsamp, ainfo, su);
   }
   PHT_STAMP(ln, 11);
   return false;
