@@ -42,7 +42,7 @@ constexpr int kRowW = 16;   /* lanes per observation */
 constexpr int kRowCap = 15; /* envelope points held by the row (point k in lane k) */
 template <int NT>
 constexpr bool row_ok() {
-  return NT > 0 && NT <= kRowW;
+  return NT > 0 && NT <= 2 * kRowW;
 }
 
 /* DPP controls (gfx9 family): quad_perm, row shifts, mirrors */
@@ -112,25 +112,76 @@ __device__ __forceinline__ double row_sum16(double v, int slot, int n) {
   return v;
 }
 
-/* lane-constant row data */
-struct RowId {
-  int rl;     /* lane in the row = envelope position */
-  int slot;   /* spectral index of this lane (gray code of rl) */
-  int ix;     /* slot, or 0 beyond n (parameter-block index) */
-  bool sv;    /* slot < n */
-  bool lead;  /* rl == 0: records the statistics */
-  double lam; /* evals(slot) (0 beyond n) */
-  double lammax;
+/* a lane's spectral values: index slot, and slot + 16 when n > 16
+ * (pht_dot16's slot r holds c_r e_r + c_{r+16} e_{r+16}) */
+template <int NT>
+struct RowV {
+  static constexpr int H = (NT > kRowW) ? 2 : 1;
+  double v[H];
 };
 
-/* per-observation state (replicated; E0 is this lane's slot) */
+/* lane-constant row data */
+template <int NT>
+struct RowId {
+  static constexpr int H = RowV<NT>::H;
+  int rl;        /* lane in the row = envelope position */
+  int slot;      /* pht_dot16 slot of this lane (gray code of rl) */
+  int ix[H];     /* spectral index slot + 16 h, or 0 beyond n (parameter-block index) */
+  bool sv[H];    /* slot + 16 h < n */
+  bool lead;     /* rl == 0: records the statistics */
+  double lam[H]; /* evals(slot + 16 h) (0 beyond n) */
+  double lammax;
+};
+template <int NT, class Par>
+__device__ __forceinline__ RowId<NT> row_id(const Par &P, int rl) {
+  RowId<NT> id;
+  id.rl = rl;
+  id.slot = rl ^ (rl >> 1);
+  id.lead = (rl == 0);
+#pragma unroll
+  for (int h = 0; h < RowId<NT>::H; h++) {
+    const int i = id.slot + kRowW * h;
+    id.sv[h] = i < NT;
+    id.ix[h] = id.sv[h] ? i : 0;
+    id.lam[h] = id.sv[h] ? P.evals(id.ix[h]) : 0.0;
+  }
+  id.lammax = lam_max(P);
+  return id;
+}
+
+/* the lane's slots of e^{lambda_i x} */
+template <int NT>
+__device__ __forceinline__ RowV<NT> rv_exp(const RowId<NT> &id, double x) {
+  RowV<NT> r;
+#pragma unroll
+  for (int h = 0; h < RowV<NT>::H; h++) r.v[h] = id.sv[h] ? pht_exp_neg(id.lam[h] * x) : 0.0;
+  return r;
+}
+/* the lane's slots of a coefficient row c(i) */
+template <int NT, class Cf>
+__device__ __forceinline__ RowV<NT> rv_coef(const RowId<NT> &id, const Cf &cf) {
+  RowV<NT> r;
+#pragma unroll
+  for (int h = 0; h < RowV<NT>::H; h++) r.v[h] = id.sv[h] ? cf(id.ix[h]) : 0.0;
+  return r;
+}
+/* pht_dot16(c, e) over the row: every lane returns it */
+template <int NT>
+__device__ __forceinline__ double rv_dot(const RowId<NT> &id, const RowV<NT> &c, const RowV<NT> &e) {
+  double p = id.sv[0] ? c.v[0] * e.v[0] : 0.0;
+  if constexpr (RowV<NT>::H > 1) p = id.sv[1] ? fma(c.v[1], e.v[1], p) : p;
+  return row_sum16(p, id.slot, NT);
+}
+
+/* per-observation state (replicated; E0 holds this lane's slots) */
+template <int NT>
 struct RowObs {
   double yt;
   int j, njump;
   bool haveE0, haveDen;
   bool fold; /* the absorb test after a jump runs at the start of the next round (row_round) */
   double den;
-  double E0; /* e^{lambda_slot yt} */
+  RowV<NT> E0; /* e^{lambda_i yt} */
 };
 
 /* the row's envelope: point rl (x, y), count and ymax (replicated) */
@@ -143,17 +194,19 @@ struct RowEnv {
 /* EcsDens on a row: log(sum_i W[j,i] e^{lambda_i (y_t - d)}) + S_jj d */
 template <int NT>
 struct RowDens {
-  const RowId &id;
+  static constexpr int H = RowV<NT>::H;
+  const RowId<NT> &id;
   int j;
   double y_t, Sjj;
-  double w;     /* W[j, slot] */
-  double E0;    /* e^{lambda_slot y_t} */
-  double El;    /* slot of the most recent evaluation */
+  RowV<NT> w;  /* W[j, i] */
+  RowV<NT> E0; /* e^{lambda_i y_t} */
+  RowV<NT> El; /* the most recent evaluation */
   double lastd;
-  __device__ __forceinline__ double sum(double e) const { return row_sum16(id.sv ? w * e : 0.0, id.slot, NT); }
+  __device__ __forceinline__ double sum(const RowV<NT> &e) const { return rv_dot(id, w, e); }
   __device__ __forceinline__ double operator()(double d) {
     const double x = y_t - d;
-    El = (d == 0.0) ? E0 : (id.sv ? pht_exp_neg(id.lam * x) : 0.0);
+    if (d == 0.0) El = E0;
+    else El = rv_exp(id, x);
     const double acc = sum(El);
     lastd = d;
     return pht_log(acc) + Sjj * d;
@@ -162,10 +215,14 @@ struct RowDens {
   __device__ __forceinline__ void init4(const double xinit[4], double acc[4]) {
     const double x3 = y_t - xinit[3];
     if (pht_ecs_init_ok(id.lammax, xinit[0], x3)) {
-      const double F = id.sv ? pht_exp_neg(id.lam * (y_t - xinit[2])) : 0.0;
-      const double T1 = F * F;
-      const double T0 = E0 * pht_exp_taylor(-id.lam * xinit[0]);
-      El = pht_exp_taylor(id.lam * x3);
+      const RowV<NT> F = rv_exp(id, y_t - xinit[2]);
+      RowV<NT> T1, T0;
+#pragma unroll
+      for (int h = 0; h < H; h++) {
+        T1.v[h] = F.v[h] * F.v[h];
+        T0.v[h] = E0.v[h] * pht_exp_taylor(-id.lam[h] * xinit[0]);
+        El.v[h] = pht_exp_taylor(id.lam[h] * x3);
+      }
       acc[2] = sum(F);
       acc[1] = sum(T1);
       acc[0] = sum(T0);
@@ -173,7 +230,7 @@ struct RowDens {
     } else {
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        El = id.sv ? pht_exp_neg(id.lam * (y_t - xinit[k])) : 0.0;
+        El = rv_exp(id, y_t - xinit[k]);
         acc[k] = sum(El);
       }
     }
@@ -413,7 +470,8 @@ __device__ __forceinline__ double row_metropolis(const RowMetroSeg &m, const WPt
 
 /* absorb test (ecs_try_absorb); true = path complete and recorded */
 template <int NT, class Sink>
-__device__ __forceinline__ bool row_try_absorb(const Par<NT> &P, const RowId &id, Lane &ln, Sink &sk, RowObs &st) {
+__device__ __forceinline__ bool row_try_absorb(const Par<NT> &P, const RowId<NT> &id, Lane &ln, Sink &sk,
+                                               RowObs<NT> &st) {
   const int j = st.j;
   bool fin = false;
   if (st.njump >= kMaxJumps) {
@@ -423,11 +481,12 @@ __device__ __forceinline__ bool row_try_absorb(const Par<NT> &P, const RowId &id
     const double y_t = st.yt;
     const double U = dev_u(ln.r);
     if (!st.haveE0) {
-      st.E0 = id.sv ? pht_exp_neg(id.lam * y_t) : 0.0;
+      st.E0 = rv_exp(id, y_t);
       st.haveE0 = true;
       st.haveDen = false;
     }
-    const double den = st.haveDen ? st.den : row_sum16(id.sv ? P.QQs(j, id.ix) * st.E0 : 0.0, id.slot, NT);
+    const double den =
+        st.haveDen ? st.den : rv_dot(id, rv_coef(id, [&](int i) { return P.QQs(j, i); }), st.E0);
     const double pab = pht_exp(fma(P.S(j, j), y_t, P.logs(j)) - pht_log(den));
     fin = (U < pab);
   }
@@ -442,14 +501,16 @@ __device__ __forceinline__ bool row_try_absorb(const Par<NT> &P, const RowId &id
 /* the first kRowSuccPre successors of state j (moveMass' candidates), read
  * at the start of the round so the loads are off the finish's chain */
 constexpr int kRowSuccPre = 2;
+template <int NT>
 struct RowSucc {
   int cnt;
   int k[kRowSuccPre];
-  double p[kRowSuccPre], qq[kRowSuccPre]; /* P[j,k], QQs[k, slot] */
+  double p[kRowSuccPre];      /* P[j,k] */
+  RowV<NT> qq[kRowSuccPre];   /* QQs[k, i] */
 };
 template <int NT>
-__device__ __forceinline__ RowSucc row_succ(const Par<NT> &P, const RowId &id, int j) {
-  RowSucc r;
+__device__ __forceinline__ RowSucc<NT> row_succ(const Par<NT> &P, const RowId<NT> &id, int j) {
+  RowSucc<NT> r;
   r.cnt = P.nsuccP(j);
 #pragma unroll
   for (int q = 0; q < kRowSuccPre; q++) {
@@ -457,15 +518,16 @@ __device__ __forceinline__ RowSucc row_succ(const Par<NT> &P, const RowId &id, i
     r.k[q] = k;
     const int kc = (q < r.cnt) ? k : 0; /* entries beyond cnt are not read */
     r.p[q] = P.P(j, kc);
-    r.qq[q] = P.QQs(kc, id.ix);
+    r.qq[q] = rv_coef(id, [&](int i) { return P.QQs(kc, i); });
   }
   return r;
 }
 
 /* ecs_jump_finish: moveMass + categorical + statistics */
 template <int NT, class Sink>
-__device__ __forceinline__ void row_jump_finish(const Par<NT> &P, const RowId &id, Lane &ln, Sink &sk, RowObs &st,
-                                                const RowDens<NT> &f, double xsamp, int ainfo, const RowSucc &su) {
+__device__ __forceinline__ void row_jump_finish(const Par<NT> &P, const RowId<NT> &id, Lane &ln, Sink &sk,
+                                                RowObs<NT> &st, const RowDens<NT> &f, double xsamp, int ainfo,
+                                                const RowSucc<NT> &su) {
   const int j = st.j;
   const double y_t = st.yt;
   if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
@@ -476,7 +538,7 @@ __device__ __forceinline__ void row_jump_finish(const Par<NT> &P, const RowId &i
   } else if (d == 0.0) {
     /* E0 already holds e^{lambda y_t} */
   } else {
-    st.E0 = id.sv ? pht_exp_neg(id.lam * x) : 0.0;
+    st.E0 = rv_exp(id, x);
   }
   st.yt = x;
   st.haveE0 = true;
@@ -487,9 +549,11 @@ __device__ __forceinline__ void row_jump_finish(const Par<NT> &P, const RowId &i
   for (int q = 0; q < NT; q++) {
     if (q < cnt) {
       const int k = (q < kRowSuccPre) ? su.k[q] : P.succP(j, q);
-      const double qq = (q < kRowSuccPre) ? su.qq[q] : P.QQs(k, id.ix);
+      RowV<NT> qq;
+      if (q < kRowSuccPre) qq = su.qq[q];
+      else qq = rv_coef(id, [&](int i) { return P.QQs(k, i); });
       const double pjk = (q < kRowSuccPre) ? su.p[q] : P.P(j, k);
-      accs[q] = row_sum16(id.sv ? qq * st.E0 : 0.0, id.slot, NT);
+      accs[q] = rv_dot(id, qq, st.E0);
       w[q] = pjk * accs[q];
       sum += w[q];
     }
@@ -534,18 +598,19 @@ __device__ __forceinline__ void row_jump_finish(const Par<NT> &P, const RowId &i
  * runs it, replicated).
  */
 template <int NT, class Sink>
-__device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId &id, Lane &ln, RowEnv &ev, EnvPrivateBig &benv,
-                                          Sink &sk, RowObs &st, bool start, bool &pend, bool &bigm, ArmsPend &pd) {
+__device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId<NT> &id, Lane &ln, RowEnv &ev,
+                                          EnvPrivateBig &benv, Sink &sk, RowObs<NT> &st, bool start, bool &pend,
+                                          bool &bigm, ArmsPend &pd) {
   const int rl = id.rl;
   const double y_t = st.yt;
   if (start && !st.haveE0) {
-    st.E0 = id.sv ? pht_exp_neg(id.lam * y_t) : 0.0;
+    st.E0 = rv_exp(id, y_t);
     st.haveE0 = true;
     st.haveDen = false;
   }
   const int j = st.j;
-  const RowSucc su = row_succ<NT>(P, id, j);
-  RowDens<NT> f{id, j, y_t, P.S(j, j), id.sv ? P.W(j, id.ix) : 0.0, st.E0, 0.0, -1.0};
+  const RowSucc<NT> su = row_succ<NT>(P, id, j);
+  RowDens<NT> f{id, j, y_t, P.S(j, j), rv_coef(id, [&](int i) { return P.W(j, i); }), st.E0, {}, -1.0};
   PHT_STAMP(ln, 1);
   double xsamp = 0.0;
   int ainfo = 0;
@@ -669,9 +734,14 @@ __device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId &id, Lan
   PHT_STAMP(ln, 9);
   /* ---- rare: envelopes beyond kRowCap, one-lane code on the private copy */
   if (big) {
+    /* every spectral index from the lane holding it: index i is slot i % 16
+     * of lane gray^-1(i % 16), half i / 16 */
     double E0f[NT];
 #pragma unroll
-    for (int i = 0; i < NT; i++) E0f[i] = row_get(st.E0, i ^ (i >> 1) ^ (i >> 2) ^ (i >> 3));
+    for (int i = 0; i < NT; i++) {
+      const int r = i % kRowW;
+      E0f[i] = row_get(st.E0.v[i / kRowW], r ^ (r >> 1) ^ (r >> 2) ^ (r >> 3));
+    }
     EcsDens<NT> f1{P, j, y_t, P.S(j, j), E0f, true, -1.0, {}, 0.0, {}};
     f1.load(id.lammax);
     const int rc = arms_step(benv, f1, pd, 0.0, xsamp, ln);
@@ -680,10 +750,13 @@ __device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId &id, Lan
       acc = true;
       bigm = false;
       f.lastd = f1.lastd;
-      double v = 0.0;
 #pragma unroll
-      for (int i = 0; i < NT; i++) v = (i == id.slot) ? f1.Elast[i] : v;
-      f.El = v;
+      for (int h = 0; h < RowV<NT>::H; h++) {
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < NT; i++) v = (i == id.slot + kRowW * h) ? f1.Elast[i] : v;
+        f.El.v[h] = v;
+      }
     }
   }
   PHT_STAMP(ln, 10);

@@ -747,19 +747,12 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
   P.d = (const PHT_LDS double *)lsm;
   P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
   P.Lr = L;
-  RowId id;
-  id.rl = (int)(threadIdx.x & (kRowW - 1));
-  id.slot = id.rl ^ (id.rl >> 1);
-  id.sv = id.slot < n;
-  id.ix = id.sv ? id.slot : 0;
-  id.lead = (id.rl == 0);
-  id.lam = id.sv ? P.evals(id.ix) : 0.0;
-  id.lammax = lam_max(P);
+  const RowId<NT> id = row_id<NT>(P, (int)(threadIdx.x & (kRowW - 1)));
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
   Lane ln;
-  RowObs st;
+  RowObs<NT> st;
   st.yt = 0.0; st.j = 0; st.njump = 0; st.haveE0 = false; st.haveDen = false; st.fold = false; st.den = 0.0;
-  st.E0 = 0.0;
+  for (int h = 0; h < RowV<NT>::H; h++) st.E0.v[h] = 0.0;
   RowEnv ev;
   ev.x = 0.0; ev.y = 0.0; ev.cnt = 0; ev.ymax = 0.0;
   EnvPrivateBig benv;

@@ -215,12 +215,13 @@ def test_longest_paths_bitexact(gpu, orc, monkeypatch, group):
 
 
 @pytest.mark.parametrize("rowk,n,cf", [(10 ** 9, 10, 0.0), (300, 10, 0.3), (10 ** 9, 3, 0.3), (10 ** 9, 5, 0.0),
-                                        (777, 15, 0.3), (1, 10, 0.0)])
+                                        (777, 15, 0.3), (1, 10, 0.0), (10 ** 9, 20, 0.3), (500, 20, 0.0)])
 def test_row_kernel_bitexact(gpu, orc, monkeypatch, rowk, n, cf):
     """The longest exact observations on 16-lane DPP rows (pht_ecs_row.h,
-    PHT_ROWK=k: positions [0, k) of the decreasing-y order; 10**9 = every
-    exact observation) give the oracle's device-spec results bit for bit,
-    per observation, next to the one-lane blocks of the same launch."""
+    PHT_ROWK=k: positions [0, k) of the decreasing-y order, at most half
+    the resident blocks' worth) give the oracle's device-spec results bit
+    for bit, per observation, next to the one-lane blocks of the same
+    launch; n = 20 puts two spectral indices in each lane."""
     monkeypatch.setenv("PHT_ROWK", str(rowk))
     S0, s0 = bd_exit(n)
     y, cen = simulate_ph(S0, s0, 3000, seed=3000 + n, censor_frac=cf)
