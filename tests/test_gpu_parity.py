@@ -83,6 +83,28 @@ def test_shard_invariance(gpu, method):
     assert np.array_equal(a[:k], parts[0][:k] + parts[1][:k])
 
 
+@pytest.mark.parametrize("n", [10, 20])
+def test_shard_invariance_rows(gpu, n):
+    """With the row blocks active (compiled n, few observations per lane),
+    three shards sum to the single-shard block exactly: each shard puts its
+    own longest paths on rows."""
+    S, s = bd_exit(n)
+    N = 9000
+    y, cen = simulate_ph(S, s, N, seed=78 + n, censor_frac=0.3)
+    zexp = P.zexp_for(y)
+    full = P.Sweeper(n, 2)
+    full.set_obs(y, cen)
+    a = full.sweep(S, s, key=(5, 7), sweep=4, zexp=zexp)
+    k = 2 * n + n * n
+    tot = np.zeros(k, dtype=a.dtype)
+    for lo, hi in ((0, 2345), (2345, 2400), (2400, N)):
+        sw = P.Sweeper(n, 2)
+        sw.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
+        tot += sw.sweep(S, s, key=(5, 7), sweep=4, zexp=zexp)[:k]
+        sw.close()
+    assert np.array_equal(a[:k], tot)
+
+
 @pytest.mark.parametrize("method,n", [(2, 4), (1, 4), (4, 4), (2, 10)])
 def test_gibbs_chain_bitexact(gpu, orc, method, n):
     """pht_gibbs_run (GPU step 1 + host Gamma update) == oracle device-variant
