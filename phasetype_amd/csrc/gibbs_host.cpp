@@ -730,10 +730,10 @@ static long exact_rowk(const pht_ctx *c) {
    * the sweep time and the more rows pay (the launcher caps rows at half
    * the resident blocks) */
   const long L = kSpreadLanes;
-  if (c->n_exact <= L) return 4096;
-  if (c->n_exact <= 2 * L) return 2048;
-  if (c->n_exact <= 5 * L) return 128;
-  return 0;
+  if (c->n_exact * 10 <= 6 * L) return 4096; /* 62.5k: 0.44 ms (1,024: 0.48; none: 0.56) */
+  if (c->n_exact <= 2 * L) return 1024;      /* 125k: 0.57 ms (4,096: 0.59; none: 0.62) */
+  if (c->n_exact <= 5 * L) return 128;       /* cfg5's 350k exact: +5 % */
+  return 0;                                  /* cfg4's 10^6: rows cost the one-lane range more (K = 64: +1 %) */
 }
 
 static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int zexp, bool debug) {
