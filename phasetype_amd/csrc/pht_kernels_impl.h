@@ -928,11 +928,15 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
   const int bpc = (a.occ > 0 && a.occ < occ) ? a.occ : occ;
   const long slots = (long)cus * bpc;
   SweepArgs b = a;
-  /* rows take at most half the resident blocks: the one-lane blocks (the
-   * rest of the range) must be resident too (a persistent block that
-   * started late would still own its claim chunks) */
-  const long rowmax = (slots / 2) * (kBlock / kRowW);
-  b.rowk = row_ok<NT>() ? std::max(0L, std::min(std::min(a.rowk, a.count), rowmax)) : 0;
+  /* rows take at most half the resident blocks, or more when every
+   * one-lane block the rest of the range wants (one lane per observation)
+   * still fits beside them: the one-lane blocks must be resident too (a
+   * persistent block that started late would still own its claim chunks) */
+  constexpr long kRows = kBlock / kRowW;
+  const long half = (slots / 2) * kRows;
+  long rk = row_ok<NT>() ? std::max(0L, std::min(a.rowk, a.count)) : 0;
+  while (rk > half && (rk + kRows - 1) / kRows + (a.count - rk + kBlock - 1) / kBlock > slots) rk -= kRows;
+  b.rowk = rk;
   b.rowblk = (int)((b.rowk + (kBlock / kRowW) - 1) / (kBlock / kRowW));
   b.begin = a.begin + b.rowk;
   b.count = a.count - b.rowk;
