@@ -53,11 +53,12 @@ def _merge_defines(defines) -> list:
     return [d for d in DEFAULT_DEFINES if d.split("=")[0] not in names] + list(defines)
 
 
-def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
-    """Compile; ``defines`` (e.g. ["PHT_DETMATH_LDS"]) and ``out`` build a
-    variant library elsewhere (tools/ab.py) without touching the default."""
+def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None, flags=()) -> str:
+    """Compile; ``defines`` (e.g. ["PHT_DETMATH_LDS"]), extra device-compile
+    ``flags`` and ``out`` build a variant library elsewhere (tools/ab.py)
+    without touching the default."""
     target = out or LIB
-    if not force and not defines and out is None and not needs_build():
+    if not force and not defines and not flags and out is None and not needs_build():
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
 
@@ -68,7 +69,7 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
         cmd = [_hipcc(), "-O3", "-fPIC", "-ffp-contract=off", f"-I{os.path.join(REPO, 'include')}", f"-I{CSRC}",
                "-Wno-pass-failed"] + [f"-D{d}" for d in _merge_defines(tuple(defines) + tuple(extra))]
         if src.endswith(".hip"):
-            cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-std=c++17"]
+            cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-std=c++17"] + list(flags)
         elif src.endswith(".cpp"):
             cmd += ["-x", "c++", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
         else:

@@ -4,7 +4,8 @@ into phasetype_amd/_variants/<name>.so, for tools/ab.py A/B runs.
 
 usage: python3 tools/build_variant.py <name> [--ref GITREF] [-D FLAG ...]
 --ref builds that revision's sources (git worktree in a temp dir); without it
-the working tree's sources are built with the given defines."""
+the working tree's sources are built with the given defines (and --flag
+hipcc flags)."""
 import argparse
 import os
 import shutil
@@ -20,6 +21,7 @@ def main():
     ap.add_argument("name")
     ap.add_argument("--ref")
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--flag", dest="flags", action="append", default=[], help="extra hipcc flag for the .hip units")
     a = ap.parse_args()
     out = os.path.join(REPO, "phasetype_amd", "_variants", a.name + ".so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
@@ -32,7 +34,7 @@ def main():
         src = tmp
     try:
         code = ("import sys; sys.path.insert(0, %r); from phasetype_amd import build as B; "
-                "B.build(force=True, defines=%r, out=%r)" % (src, tuple(a.defines), out))
+                "B.build(force=True, defines=%r, out=%r, flags=%r)" % (src, tuple(a.defines), out, tuple(a.flags)))
         subprocess.run([sys.executable, "-c", code], check=True)
     finally:
         if tmp:
