@@ -1,5 +1,5 @@
-"""CPU, world_size 2 and 3 over gloo: the multi-process sharding of
-phasetype_amd/dist.py (the code bench.py runs over RCCL on the GPUs).
+"""CPU, world_size 2, 3 and 8 (the driver's largest node) over gloo: the
+multi-process sharding of phasetype_amd/dist.py (the code bench.py runs over RCCL on the GPUs).
 
 Each rank sweeps its shard_range() of the observations with the device
 specification (oracle "dev" variant, global observation ids = obs0 offsets,
@@ -71,7 +71,7 @@ def _worker(rank, world, port, cases):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_sweeps_sum_to_single_sweep(orc, world):
     import torch.multiprocessing as mp
 
