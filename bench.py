@@ -32,7 +32,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 import phasetype_amd as P  # noqa: E402
-from phasetype_amd.dist import make_stats_allreduce, max_over_ranks, shard_range, sum_over_ranks  # noqa: E402
+from phasetype_amd.dist import attach_rccl, make_stats_allreduce, max_over_ranks, shard_range, sum_over_ranks  # noqa: E402
 from phasetype_amd.synth import DATA_KEY, bd_exit, bd_exit_structure, simulate_ph  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
@@ -134,9 +134,16 @@ def main():
     sw.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
     Cm = np.ones(T.shape)
 
+    # On the GPUs the statistics block is summed by an RCCL all-reduce inside
+    # the library, on the sweep's stream (attach_rccl); PHT_STATS_REDUCE=
+    # callback (and gloo) use the host callback through torch.distributed.
+    in_lib = dist is not None and coll_dev != "cpu" and os.environ.get("PHT_STATS_REDUCE", "rccl") == "rccl"
     reduce = None
     if dist is not None:
-        reduce = make_stats_allreduce(dist, P.stats_len(n), device=coll_dev)
+        if in_lib:
+            attach_rccl(sw, dist, coll_dev)
+        else:
+            reduce = make_stats_allreduce(dist, P.stats_len(n), device=coll_dev)
 
     def sync():
         if dist is not None:
@@ -170,6 +177,8 @@ def main():
         zexp_w = P.zexp_for(np.array([tot]))
         sw2 = P.Sweeper(n, method, 1, device=local)
         sw2.set_obs(yw, cw, obs0=rank * N)
+        if in_lib:
+            attach_rccl(sw2, dist, coll_dev)
         P.set_seed(20241009)
         warm = sw2.gibbs(args.warmup + 1, method, nu, zeta, T, Cm, zexp_w, reduce=reduce)
         sync()
@@ -216,7 +225,8 @@ def main():
                     f"censored fraction {args.censor}, Philox key 0x{DATA_KEY:x}",
             "config": {"workload": f"{cfg_name}: phtMCMC2 {args.method}, n={n} states, m={m} parameters, "
                                    f"N={N} obs ({args.censor:.0%} censored), priors nu=1+50*theta, zeta=50, mhit=1",
-                       "n": n, "N": N, "method": args.method, "parallelism": f"obs-shard x{world}"},
+                       "n": n, "N": N, "method": args.method, "parallelism": f"obs-shard x{world}",
+                       "stats_reduce": "rccl-in-stream" if in_lib else ("host-callback" if dist is not None else "none")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kernel_ms,

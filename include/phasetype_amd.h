@@ -80,6 +80,16 @@ int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double *nu, const
                   const double *C, int zexp, int silent, const double *start, double *res, pht_reduce_fn reduce,
                   void *reduce_user, double *kernel_ms_total);
 
+/* Multi-process runs without a host callback: every sweep's statistics
+ * block on this context is summed over `nranks` processes by an RCCL
+ * all-reduce (uint64, in place) on the context's stream, before its copy to
+ * the host; pht_gibbs_run then takes reduce = NULL.  One rank calls
+ * pht_rccl_unique_id and broadcasts the 128 bytes; every rank attaches with
+ * the same id.  RCCL is loaded at run time (librccl.so.1).  No reference
+ * counterpart: the reference is single-process (src/PHT_MCMC_Aslett.c:325-337). */
+int pht_rccl_unique_id(unsigned char *id128);
+int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id128, int nranks, int rank);
+
 /* Independent chains at once (no reference counterpart —
  * the reference runs one chain per LJMA_Gibbs call, src/PHT_MCMC_Aslett.c:104):
  * chain c on ctxs[c] (one context each, same n/method/mhit, observations set),
@@ -89,7 +99,8 @@ int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double *nu, const
  * reads start[c*m .. c*m+m-1]) or start[0] < 0 — the length is not checked
  * here, so a caller holding one m-vector must repeat it per chain (the
  * Python mirror phasetype_amd.gibbs_chains broadcasts and validates it).
- * Standalone builds only (fails inside R). */
+ * Standalone builds only (fails inside R), and not on contexts with an RCCL
+ * communicator attached. */
 int pht_gibbs_run_chains(pht_ctx **ctxs, int nchains, const uint32_t *seeds, int it, int method, int m,
                          const double *nu, const double *zeta, const int *T, const double *C, int zexp,
                          const double *start, double *res, double *kernel_ms_max);

@@ -47,7 +47,7 @@ EXPORTS = [
     "pht_unif_rand", "pht_rgamma", "pht_in_R", "pht_set_verbose", "pht_zexp", "pht_params_bytes", "pht_stats_len",
     "pht_build_params", "pht_ctx_create", "pht_ctx_destroy", "pht_ctx_set_obs", "pht_ctx_sweep",
     "pht_ctx_sweep_debug", "pht_ctx_last_kernel_ms", "pht_ctx_flagged_obs", "pht_gibbs_run",
-    "pht_gibbs_run_chains",
+    "pht_gibbs_run_chains", "pht_rccl_unique_id", "pht_ctx_attach_rccl",
 ]
 
 
@@ -100,6 +100,8 @@ def load(build_if_needed: bool = True) -> C.CDLL:
                                 _dp, _dp, C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]
     L.pht_gibbs_run_chains.argtypes = [C.POINTER(C.c_void_p), C.c_int, _up, C.c_int, C.c_int, C.c_int, _dp, _dp,
                                        _ip, _dp, C.c_int, _dp, _dp, C.POINTER(C.c_double)]
+    L.pht_rccl_unique_id.argtypes = [C.c_void_p]
+    L.pht_ctx_attach_rccl.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_int]
     L.LJMA_Gibbs.argtypes = [_ip, _ip, _ip, _ip, _ip, _dp, _dp, _ip, _dp, _dp, _ip, _ip, _dp, _ip, _dp]
     p, pre = _lapack_path()
     if L.pht_bind_lapack(p.encode(), pre.encode()) != 0:
@@ -137,6 +139,18 @@ def split_stats(st, n):
     B = st[n:2 * n]
     N = st[2 * n:2 * n + n * n].reshape(n, n).T  # N[i + j n] -> [i, j]
     return zq, B, N, st[2 * n + n * n:]
+
+
+RCCL_ID_BYTES = 128
+
+
+def rccl_unique_id() -> bytes:
+    """A fresh RCCL unique id (one rank creates it and broadcasts it)."""
+    L = load()
+    buf = C.create_string_buffer(RCCL_ID_BYTES)
+    if L.pht_rccl_unique_id(buf) != 0:
+        raise _err(L)
+    return buf.raw
 
 
 class Sweeper:
@@ -179,6 +193,16 @@ class Sweeper:
             raise _err(self.L)
         return dict(stats=out, B=B, pre=pre, flags=fl, ndraw=nd, zq=zq.reshape(l, n),
                     N=N.reshape(l, n, n).transpose(0, 2, 1))
+
+    def attach_rccl(self, uid: bytes, nranks: int, rank: int) -> None:
+        """Sum every sweep's statistics block over ``nranks`` processes with
+        an RCCL all-reduce on this shard's stream (pht_ctx_attach_rccl);
+        ``uid`` = rccl_unique_id() of one rank, the same on all.  gibbs()
+        then needs no ``reduce``."""
+        if len(uid) != RCCL_ID_BYTES:
+            raise ValueError(f"RCCL unique id must be {RCCL_ID_BYTES} bytes, got {len(uid)}")
+        if self.L.pht_ctx_attach_rccl(self.ctx, uid, nranks, rank) != 0:
+            raise _err(self.L)
 
     def last_kernel_ms(self) -> float:
         return self.L.pht_ctx_last_kernel_ms(self.ctx)

@@ -20,6 +20,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <rccl/rccl.h>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -380,6 +381,7 @@ struct pht_ctx {
   struct ChainGroup *grp = nullptr; /* pht_gibbs_run_chains: exact ECS launched with the other chains */
   int gidx = -1;
   long long flagged = 0; /* flagged observation-sweeps of the last Gibbs run (node-wide) */
+  ncclComm_t comm = nullptr; /* pht_ctx_attach_rccl: stats summed over ranks on `stream` */
 };
 
 /* lanes of the persistent ECS grid on an MI355X (256 CUs x 2 blocks x 256) */
@@ -581,6 +583,91 @@ static void ctx_free_dbg(pht_ctx *c) {
   c->dbg_cap = 0;
 }
 
+/*
+ * RCCL bound at run time (dlopen), so the library loads where RCCL is absent
+ * (inside R on a single GPU) and only multi-process runs need it.  Replaces
+ * the per-sweep host callback (pht_reduce_fn) with an all-reduce on the device
+ * copy of the statistics block, on the sweep's stream: no host round trip
+ * between the kernels and the sum.  The reference has no distributed mode
+ * (its observation loop is src/PHT_MCMC_Aslett.c:325-337).
+ */
+struct RcclApi {
+  bool ok = false;
+  ncclResult_t (*getUniqueId)(ncclUniqueId *) = nullptr;
+  ncclResult_t (*commInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*allReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+  const char *(*errStr)(ncclResult_t) = nullptr;
+};
+static RcclApi &rccl() {
+  static RcclApi a;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    a.getUniqueId = (decltype(a.getUniqueId))dlsym(h, "ncclGetUniqueId");
+    a.commInitRank = (decltype(a.commInitRank))dlsym(h, "ncclCommInitRank");
+    a.allReduce = (decltype(a.allReduce))dlsym(h, "ncclAllReduce");
+    a.commDestroy = (decltype(a.commDestroy))dlsym(h, "ncclCommDestroy");
+    a.errStr = (decltype(a.errStr))dlsym(h, "ncclGetErrorString");
+    a.ok = a.getUniqueId && a.commInitRank && a.allReduce && a.commDestroy && a.errStr;
+  });
+  return a;
+}
+static void rccl_destroy(ncclComm_t comm) {
+  if (rccl().ok) (void)rccl().commDestroy(comm);
+}
+
+extern "C" int pht_rccl_unique_id(unsigned char *id) {
+  if (!id) {
+    set_err("pht_rccl_unique_id: null buffer");
+    return -1;
+  }
+  if (!rccl().ok) {
+    set_err("RCCL (librccl.so.1) could not be loaded");
+    return -1;
+  }
+  ncclUniqueId u;
+  const ncclResult_t r = rccl().getUniqueId(&u);
+  if (r != ncclSuccess) {
+    set_err("ncclGetUniqueId failed: %s", rccl().errStr(r));
+    return -1;
+  }
+  memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+  return 0;
+}
+
+extern "C" int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id, int nranks, int rank) {
+  if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) {
+    set_err("pht_ctx_attach_rccl: need a context, a unique id and 0 <= rank < nranks");
+    return -1;
+  }
+  if (c->comm) {
+    set_err("pht_ctx_attach_rccl: a communicator is already attached");
+    return -1;
+  }
+  if (!rccl().ok) {
+    set_err("RCCL (librccl.so.1) could not be loaded");
+    return -1;
+  }
+  if (hipSetDevice(c->device) != hipSuccess) {
+    set_err("pht_ctx_attach_rccl: device %d", c->device);
+    return -1;
+  }
+  ncclUniqueId u;
+  memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t comm = nullptr;
+  const ncclResult_t r = rccl().commInitRank(&comm, nranks, u, rank);
+  if (r != ncclSuccess) {
+    set_err("ncclCommInitRank (rank %d of %d) failed: %s", rank, nranks, rccl().errStr(r));
+    return -1;
+  }
+  c->comm = comm;
+  return 0;
+}
+
 extern "C" int pht_device_count(void) {
   int c = 0;
   if (hipGetDeviceCount(&c) != hipSuccess) return 0;
@@ -640,6 +727,7 @@ extern "C" void pht_ctx_destroy(pht_ctx *c) {
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->evf) (void)hipEventDestroy(c->evf);
   if (c->evj) (void)hipEventDestroy(c->evj);
+  if (c->comm) rccl_destroy(c->comm);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -829,6 +917,15 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     HIPCHK(pht_launch_sweep(&a, c->method, debug ? 1 : 0, c->stream));
   }
   HIPCHK(hipEventRecord(c->ev1, c->stream));
+  if (c->comm) {
+    /* multi-process: the block summed over all ranks in place, on the sweep's
+     * stream, before the one copy to the host (pht_ctx_attach_rccl) */
+    const ncclResult_t r = rccl().allReduce(c->d_stats, c->d_stats, (size_t)sl, ncclUint64, ncclSum, c->comm, c->stream);
+    if (r != ncclSuccess) {
+      set_err("RCCL all-reduce of the statistics failed: %s", rccl().errStr(r));
+      return -1;
+    }
+  }
   HIPCHK(hipMemcpyAsync(c->h_stats, c->d_stats, sizeof(unsigned long long) * sl, hipMemcpyDeviceToHost, c->stream));
   return 0;
 }
@@ -1113,6 +1210,11 @@ extern "C" int pht_gibbs_run_chains(pht_ctx **ctxs, int nchains, const uint32_t 
     set_err("pht_gibbs_run_chains is not available inside R (host threads)");
     return -1;
   }
+  for (int c = 0; c < nchains; c++)
+    if (!ctxs[c] || ctxs[c]->comm) {
+      set_err("pht_gibbs_run_chains: context %d is null or has an RCCL communicator attached", c);
+      return -1;
+    }
   /* exact ECS ranges of all chains in one launch per sweep, when the chains
    * share a device and n (PHT_CHAINS_LAUNCH=streams: one launch per chain) */
   ChainGroup *grp = nullptr;

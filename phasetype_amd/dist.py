@@ -52,6 +52,22 @@ def make_stats_allreduce(dist, n_words: int, device: str = "cpu"):
     return reduce
 
 
+def attach_rccl(sweeper, dist, device: str) -> None:
+    """The in-library alternative to make_stats_allreduce on GPUs: rank 0
+    makes an RCCL unique id, torch.distributed broadcasts it, and every
+    rank's Sweeper sums its statistics block with an RCCL all-reduce on its
+    own sweep stream (no host callback, no staging copies per sweep)."""
+    import torch
+
+    from . import RCCL_ID_BYTES, rccl_unique_id
+
+    t = torch.zeros(RCCL_ID_BYTES, dtype=torch.uint8, device=device)
+    if dist.get_rank() == 0:
+        t.copy_(torch.frombuffer(bytearray(rccl_unique_id()), dtype=torch.uint8))
+    dist.broadcast(t, 0)
+    sweeper.attach_rccl(bytes(t.cpu().numpy().tobytes()), dist.get_world_size(), dist.get_rank())
+
+
 def max_over_ranks(dist, values, device: str = "cpu"):
     """Element-wise max of a few floats over ranks (bench timing)."""
     import torch
