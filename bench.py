@@ -86,8 +86,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=10)
-    ap.add_argument("--N", type=int, default=1_000_000)
+    ap.add_argument("--n", "--states", dest="n", type=int, default=10)
+    ap.add_argument("--N", "--obs", dest="N", type=int, default=1_000_000)
     ap.add_argument("--method", default="ECS", choices=["ECS", "MHRS", "DCS"])
     ap.add_argument("--censor", type=float, default=0.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
