@@ -382,6 +382,8 @@ struct pht_ctx {
   int gidx = -1;
   long long flagged = 0; /* flagged observation-sweeps of the last Gibbs run (node-wide) */
   ncclComm_t comm = nullptr; /* pht_ctx_attach_rccl: stats summed over ranks on `stream` */
+  bool stats_zero = false;   /* d_stats zeroed on `stream` after the last sweep's copy */
+  hipEvent_t evd = nullptr;  /* the statistics copy to the host is done */
 };
 
 /* lanes of the persistent ECS grid on an MI355X (256 CUs x 2 blocks x 256) */
@@ -706,7 +708,8 @@ extern "C" pht_ctx *pht_ctx_create(int device, int n, int method, int mhit) {
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->evf, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->evj, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->evj, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evd, hipEventDisableTiming) != hipSuccess) {
     set_err("device %d: HIP allocation failed", device);
     delete c;
     return nullptr;
@@ -727,6 +730,7 @@ extern "C" void pht_ctx_destroy(pht_ctx *c) {
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->evf) (void)hipEventDestroy(c->evf);
   if (c->evj) (void)hipEventDestroy(c->evj);
+  if (c->evd) (void)hipEventDestroy(c->evd);
   if (c->comm) rccl_destroy(c->comm);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -829,7 +833,12 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   const int pb = make_layout(c->n).bytes();
   const int sl = stats_len(c->n);
   HIPCHK(hipMemcpyAsync(c->d_params, c->h_params, pb, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * sl, c->stream));
+  /* the block is zeroed at the end of the previous sweep, after its copy to
+   * the host (off the critical path: it runs while the host does the Gamma
+   * update); only the first sweep, or one after a failed enqueue, zeroes it
+   * here */
+  if (!c->stats_zero) HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * sl, c->stream));
+  c->stats_zero = false;
   SweepArgs a;
   memset(&a, 0, sizeof a);
   a.params = c->d_params;
@@ -927,12 +936,15 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     }
   }
   HIPCHK(hipMemcpyAsync(c->h_stats, c->d_stats, sizeof(unsigned long long) * sl, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipEventRecord(c->evd, c->stream)); /* ctx_wait waits for this, not for the zeroing */
+  HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * sl, c->stream));
+  c->stats_zero = true;
   return 0;
 }
 
 static int ctx_wait(pht_ctx *c) {
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipEventSynchronize(c->evd));
   HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
   if (c->method == kMethodMHRS && c->d_mcnt && getenv("PHT_MHRS_COUNTS")) {
     /* diagnostics: tasks still unresolved after MHRS search rounds 0..4 */
