@@ -1,6 +1,6 @@
 #!/bin/bash
 # bench.py at every BASELINE.json config that fits one GPU (no CPU baseline):
-# cfg2 n=5 N=1e4 ECS; cfg3 n=20 N=1e5 ECS; cfg4 n=10 N=1e6 ECS + MHRS;
+# cfg1 n=3 N=200 ECS (the CPU-plumbing config, 1000 sweeps); cfg2 n=5 N=1e4 ECS; cfg3 n=20 N=1e5 ECS; cfg4 n=10 N=1e6 ECS + MHRS;
 # cfg5 n=15 N=5e5 30% censored, MHRS / DCS / ECS.  usage: tools/gpu_configs.sh <tag>
 set -o pipefail
 TAG=${1:-cfgs}
@@ -8,6 +8,7 @@ O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $O
 cd $GRAFT_REPO_ROOT
 run() { local name=$1; shift; timeout -k 10 240 python3 bench.py --no-cpu-baseline "$@" > $O/$name.json 2> $O/$name.err || { echo "$name failed"; exit 1; }; echo "$name ok"; }
+run cfg1_ecs --n 3 --N 200 --steps 1000
 run cfg2_ecs --n 5 --N 10000 --steps 50
 run cfg3_ecs --n 20 --N 100000 --steps 20
 run cfg4_ecs --n 10 --N 1000000 --steps 20
