@@ -44,23 +44,17 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n, y, cen, T, nu, zeta, target_s=15.0):
-    """The reference's own C (oracle/_ref/libpht_ref.so, compiled in place from
-    /root/reference/src) timed single-threaded on a bounded sample of the same
-    workload; falls back to the bit-exact restatement (oracle ref variant)."""
+def cpu_baseline(n, y, cen, T, nu, zeta, method=2, target_s=15.0):
+    """The CPU restatement of the reference (oracle/, "ref" variant: R's
+    stream, libm, the reference's arithmetic order; kind "port") timed
+    single-threaded on a bounded sample of the same workload.  The reference
+    itself needs R and cannot be built in this image."""
     from oracle import oracle as O
 
-    kind = "reference"
-    try:
-        lib = O.RefLib()
-        run = lambda it, yy, cc: lib.gibbs(it, 1, 2, n, nu, zeta, T.reshape(-1, order="F"),  # noqa: E731
-                                           np.ones(T.size), yy, cc)
-    except Exception as e:  # noqa: BLE001
-        log(f"[bench] reference oracle unavailable ({e}); timing the restatement")
-        kind = "port"
-        lib = O.OracleLib()
-        run = lambda it, yy, cc: lib.gibbs(0, it, 1, 2, n, nu, zeta, T.reshape(-1, order="F"),  # noqa: E731
-                                           np.ones(T.size), yy, cc)
+    kind = "port"
+    lib = O.OracleLib()
+    run = lambda it, yy, cc: lib.gibbs(0, it, 1, method, n, nu, zeta, T.reshape(-1, order="F"),  # noqa: E731
+                                       np.ones(T.size), yy, cc)
     lib.set_seed(1)
     probe = 20000
     t0 = time.perf_counter()
@@ -132,18 +126,32 @@ def main():
     lo, hi = shard_range(N, rank, world)
     sw = P.Sweeper(n, method, 1, device=local)
     sw.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
+    sw.set_global_count(N)  # every sweep checks that all N observations were sampled
     Cm = np.ones(T.shape)
 
     # On the GPUs the statistics block is summed by an RCCL all-reduce inside
     # the library, on the sweep's stream (attach_rccl); PHT_STATS_REDUCE=
     # callback (and gloo) use the host callback through torch.distributed.
+    # attach_rccl self-tests the library's all-reduce against torch.distributed
+    # on every rank; if that fails the run falls back to the host callback.
     in_lib = dist is not None and coll_dev != "cpu" and os.environ.get("PHT_STATS_REDUCE", "rccl") == "rccl"
     reduce = None
+    reduce_note = "none"
     if dist is not None:
+        if in_lib and not attach_rccl(sw, dist, coll_dev):
+            log("[bench] in-library RCCL all-reduce failed its self-test; using the host callback")
+            in_lib = False
+            sw.close()
+            sw = P.Sweeper(n, method, 1, device=local)
+            sw.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
+            sw.set_global_count(N)
+            reduce_note = "host-callback (rccl self-test failed)"
         if in_lib:
-            attach_rccl(sw, dist, coll_dev)
+            reduce_note = "rccl-in-stream (self-tested)"
         else:
             reduce = make_stats_allreduce(dist, P.stats_len(n), device=coll_dev)
+            if reduce_note == "none":
+                reduce_note = "host-callback"
 
     def sync():
         if dist is not None:
@@ -177,8 +185,9 @@ def main():
         zexp_w = P.zexp_for(np.array([tot]))
         sw2 = P.Sweeper(n, method, 1, device=local)
         sw2.set_obs(yw, cw, obs0=rank * N)
-        if in_lib:
-            attach_rccl(sw2, dist, coll_dev)
+        sw2.set_global_count(N * world)
+        if in_lib and not attach_rccl(sw2, dist, coll_dev):
+            raise SystemExit("in-library RCCL all-reduce passed its self-test once, then failed it")
         P.set_seed(20241009)
         warm = sw2.gibbs(args.warmup + 1, method, nu, zeta, T, Cm, zexp_w, reduce=reduce)
         sync()
@@ -226,7 +235,7 @@ def main():
             "config": {"workload": f"{cfg_name}: phtMCMC2 {args.method}, n={n} states, m={m} parameters, "
                                    f"N={N} obs ({args.censor:.0%} censored), priors nu=1+50*theta, zeta=50, mhit=1",
                        "n": n, "N": N, "method": args.method, "parallelism": f"obs-shard x{world}",
-                       "stats_reduce": "rccl-in-stream" if in_lib else ("host-callback" if dist is not None else "none")},
+                       "stats_reduce": reduce_note},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kernel_ms,
@@ -243,7 +252,7 @@ def main():
             line["weak_scaling"] = weak
         if world == 1 and not args.no_cpu_baseline:
             try:
-                line["cpu_baseline"] = cpu_baseline(n, y, cen, T, nu, zeta)
+                line["cpu_baseline"] = cpu_baseline(n, y, cen, T, nu, zeta, method)
             except Exception as e:  # noqa: BLE001
                 log(f"[bench] cpu baseline failed: {e}")
                 line["cpu_baseline"] = None
@@ -253,7 +262,7 @@ def main():
                 import subprocess
 
                 cmd = [sys.executable, "-m", "oracle.cpu_best", "--n", str(n), "--N", str(N), "--censor",
-                       str(args.censor), "--workers", "16", "--seconds", "10"]
+                       str(args.censor), "--workers", "16", "--seconds", "10", "--method", str(method)]
                 out = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=180, check=True).stdout
                 line["cpu_best"] = json.loads(out.strip().splitlines()[-1])
                 line["cpu_best"]["ratio_gpu_over_cpu_best"] = line["value"] / line["cpu_best"]["value"]

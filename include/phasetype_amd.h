@@ -72,9 +72,20 @@ float pht_ctx_last_kernel_ms(pht_ctx *c);
  * contributed its last attempt.  No reference counterpart (its loops are
  * unbounded); a warning is also printed once per run. */
 long long pht_ctx_flagged_obs(pht_ctx *c);
+/* Observations over ALL shards of a multi-process run (this context's shard
+ * included).  pht_gibbs_run checks every sweep that the node-wide statistics
+ * account for exactly this many observations, and fails the run otherwise
+ * (single process: the check uses the context's own count, always on).  No
+ * reference counterpart (the reference has one process and no such failure
+ * mode, src/PHT_MCMC_Aslett.c:325-337). */
+int pht_ctx_set_global_count(pht_ctx *c, long long total);
 
 /* Gibbs loop over one shard; reduce(stats, len, user) must sum the int64
- * block across all shards (return 0 on success). */
+ * block across all shards (return 0 on success), or NULL (single process, or
+ * an RCCL communicator attached: passing both is an error, the block would be
+ * summed twice).  Every sweep is checked: the node-wide processed count must
+ * equal the observations (see pht_ctx_set_global_count), and the fixed-point
+ * z sums must not overflow int64; either failure ends the run with an error. */
 typedef int (*pht_reduce_fn)(long long *stats, int len, void *user);
 int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double *nu, const double *zeta, const int *T,
                   const double *C, int zexp, int silent, const double *start, double *res, pht_reduce_fn reduce,
@@ -89,6 +100,10 @@ int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double *nu, const
  * counterpart: the reference is single-process (src/PHT_MCMC_Aslett.c:325-337). */
 int pht_rccl_unique_id(unsigned char *id128);
 int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id128, int nranks, int rank);
+/* In-place sum of buf[len] (host int64) over the attached communicator, on
+ * the context's stream: the all-reduce a sweep runs on its statistics block,
+ * exposed so the caller can check it against its own collective. */
+int pht_ctx_rccl_allreduce(pht_ctx *c, long long *buf, int len);
 
 /* Independent chains at once (no reference counterpart —
  * the reference runs one chain per LJMA_Gibbs call, src/PHT_MCMC_Aslett.c:104):

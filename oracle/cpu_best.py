@@ -1,18 +1,18 @@
 """oracle/cpu_best.py — TEST INFRASTRUCTURE ONLY (bench.py's CPU comparison).
 
-The "best CPU" line of SURVEY.md §8(d): the reference's own C
-(oracle/_ref/libpht_ref.so, LJMA_Gibbs as R's .C calls it) on W host cores at
+The "best CPU" line of SURVEY.md §8(d): the CPU restatement of the reference
+(oracle/, "ref" variant, LJMA_Gibbs as R's .C calls it) on W host cores at
 once, the observations split W ways.  The reference is single-threaded and
 its per-sweep work is linear in the observations, so W processes each running
-the reference over 1/W of a bounded sample measure what an ideal
+the restatement over 1/W of a bounded sample measure what an ideal
 observation-parallel CPU port would reach: value = W x (sweeps/s over
 N_sample / W) x N_sample / N, with the wall time of the slowest worker.  The
 per-sweep reduction such a port needs is not charged (it favours the CPU).
 
 Run as a child process (bench.py does: the GPU process never forks workers):
     python3 -m oracle.cpu_best --n 10 --N 1000000 --workers 16 --seconds 10
-Prints one JSON object.  Falls back to the bit-exact restatement (oracle "ref"
-variant) when the reference build is absent.
+Prints one JSON object.  (The reference itself needs R and cannot be built in
+this image)
 """
 from __future__ import annotations
 
@@ -31,23 +31,19 @@ sys.path.insert(0, os.path.dirname(HERE))
 from phasetype_amd.synth import DATA_KEY, bd_exit, bd_exit_structure, simulate_ph  # noqa: E402
 
 
-def _runner(n):
+def _runner(n, method=2):
     from oracle import oracle as O
 
     T, theta = bd_exit_structure(n)
     nu, zeta = 1.0 + 50.0 * theta, np.full(len(theta), 50.0)
     Tf = T.reshape(-1, order="F")
-    try:
-        lib = O.RefLib()
-        return "reference", lambda it, y, c: lib.gibbs(it, 1, 2, n, nu, zeta, Tf, np.ones(T.size), y, c), lib
-    except Exception:  # noqa: BLE001
-        lib = O.OracleLib()
-        return "port", lambda it, y, c: lib.gibbs(0, it, 1, 2, n, nu, zeta, Tf, np.ones(T.size), y, c), lib
+    lib = O.OracleLib()
+    return "port", lambda it, y, c: lib.gibbs(0, it, 1, method, n, nu, zeta, Tf, np.ones(T.size), y, c), lib
 
 
 def _worker(args):
-    n, y, c, sweeps, t_start = args
-    _, run, lib = _runner(n)
+    n, method, y, c, sweeps, t_start = args
+    _, run, lib = _runner(n, method)
     lib.set_seed(3)
     while time.time() < t_start:  # common start, so the slowest worker's wall is the job's
         time.sleep(0.001)
@@ -63,11 +59,12 @@ def main():
     ap.add_argument("--censor", type=float, default=0.0)
     ap.add_argument("--workers", type=int, default=16)
     ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--method", type=int, default=2)
     a = ap.parse_args()
     S, s = bd_exit(a.n)
     y, cen = simulate_ph(S, s, a.N, seed=DATA_KEY, censor_frac=a.censor)
     W = max(1, min(a.workers, os.cpu_count() or 1))
-    kind, run, lib = _runner(a.n)
+    kind, run, lib = _runner(a.n, a.method)
     lib.set_seed(1)
     probe = min(len(y), 20000)
     t0 = time.perf_counter()
@@ -77,7 +74,7 @@ def main():
     per_w = int(min(len(y) // W, max(2000, a.seconds / max(per_obs_sweep * 5, 1e-12))))
     sweeps = max(2, min(50, int(a.seconds / max(per_obs_sweep * per_w, 1e-12))))
     nsamp = per_w * W
-    jobs = [(a.n, np.ascontiguousarray(y[k * per_w:(k + 1) * per_w]), np.ascontiguousarray(cen[k * per_w:(k + 1) * per_w]),
+    jobs = [(a.n, a.method, np.ascontiguousarray(y[k * per_w:(k + 1) * per_w]), np.ascontiguousarray(cen[k * per_w:(k + 1) * per_w]),
              sweeps, time.time() + 1.0) for k in range(W)]
     with mp.get_context("fork").Pool(W) as pool:
         walls = pool.map(_worker, jobs)

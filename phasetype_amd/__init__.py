@@ -46,8 +46,8 @@ EXPORTS = [
     "LJMA_Gibbs", "R_init_PhaseType", "pht_last_error", "pht_device_count", "pht_bind_lapack", "pht_set_seed",
     "pht_unif_rand", "pht_rgamma", "pht_in_R", "pht_set_verbose", "pht_zexp", "pht_params_bytes", "pht_stats_len",
     "pht_build_params", "pht_ctx_create", "pht_ctx_destroy", "pht_ctx_set_obs", "pht_ctx_sweep",
-    "pht_ctx_sweep_debug", "pht_ctx_last_kernel_ms", "pht_ctx_flagged_obs", "pht_gibbs_run",
-    "pht_gibbs_run_chains", "pht_rccl_unique_id", "pht_ctx_attach_rccl",
+    "pht_ctx_sweep_debug", "pht_ctx_last_kernel_ms", "pht_ctx_flagged_obs", "pht_ctx_set_global_count", "pht_gibbs_run",
+    "pht_gibbs_run_chains", "pht_rccl_unique_id", "pht_ctx_attach_rccl", "pht_ctx_rccl_allreduce",
 ]
 
 
@@ -96,12 +96,14 @@ def load(build_if_needed: bool = True) -> C.CDLL:
     L.pht_ctx_last_kernel_ms.argtypes = [C.c_void_p]
     L.pht_ctx_flagged_obs.restype = C.c_longlong
     L.pht_ctx_flagged_obs.argtypes = [C.c_void_p]
+    L.pht_ctx_set_global_count.argtypes = [C.c_void_p, C.c_longlong]
     L.pht_gibbs_run.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _dp, C.c_int, C.c_int,
                                 _dp, _dp, C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]
     L.pht_gibbs_run_chains.argtypes = [C.POINTER(C.c_void_p), C.c_int, _up, C.c_int, C.c_int, C.c_int, _dp, _dp,
                                        _ip, _dp, C.c_int, _dp, _dp, C.POINTER(C.c_double)]
     L.pht_rccl_unique_id.argtypes = [C.c_void_p]
     L.pht_ctx_attach_rccl.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_int]
+    L.pht_ctx_rccl_allreduce.argtypes = [C.c_void_p, _lp, C.c_int]
     L.LJMA_Gibbs.argtypes = [_ip, _ip, _ip, _ip, _ip, _dp, _dp, _ip, _dp, _dp, _ip, _ip, _dp, _ip, _dp]
     p, pre = _lapack_path()
     if L.pht_bind_lapack(p.encode(), pre.encode()) != 0:
@@ -194,6 +196,13 @@ class Sweeper:
         return dict(stats=out, B=B, pre=pre, flags=fl, ndraw=nd, zq=zq.reshape(l, n),
                     N=N.reshape(l, n, n).transpose(0, 2, 1))
 
+    def set_global_count(self, total: int) -> None:
+        """Observations over all shards of a multi-process run: every sweep of
+        gibbs() then checks the reduced statistics account for exactly that
+        many (pht_ctx_set_global_count)."""
+        if self.L.pht_ctx_set_global_count(self.ctx, int(total)) != 0:
+            raise _err(self.L)
+
     def attach_rccl(self, uid: bytes, nranks: int, rank: int) -> None:
         """Sum every sweep's statistics block over ``nranks`` processes with
         an RCCL all-reduce on this shard's stream (pht_ctx_attach_rccl);
@@ -202,6 +211,14 @@ class Sweeper:
         if len(uid) != RCCL_ID_BYTES:
             raise ValueError(f"RCCL unique id must be {RCCL_ID_BYTES} bytes, got {len(uid)}")
         if self.L.pht_ctx_attach_rccl(self.ctx, uid, nranks, rank) != 0:
+            raise _err(self.L)
+
+    def rccl_allreduce(self, buf: np.ndarray) -> None:
+        """In-place sum of an int64 vector over the attached communicator
+        (the same all-reduce a sweep runs on its statistics block)."""
+        if buf.dtype != np.int64 or not buf.flags.c_contiguous:
+            raise ValueError("rccl_allreduce needs a contiguous int64 array")
+        if self.L.pht_ctx_rccl_allreduce(self.ctx, buf, len(buf)) != 0:
             raise _err(self.L)
 
     def last_kernel_ms(self) -> float:

@@ -25,7 +25,7 @@ UNITS = [("pht_kernels_nt.hip", (f"PHT_NT={k}",)) for k in KERNEL_NTS] + [
     ("pht_dispatch.hip", ()), ("gibbs_host.cpp", ()), ("rstream.c", ())]
 SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = ["pht_device.h", "pht_env.h", "pht_kernels.h", "pht_kernels_impl.h", "pht_layout.h", "rstream.h",
-           "pht_ecs_round.h", "pht_ecs_group.h", "pht_ecs_row.h", "pht_dcs_round.h", "pht_cens_round.h"]
+           "pht_ecs_round.h", "pht_ecs_row.h", "pht_dcs_round.h", "pht_cens_round.h"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 DEFAULT_DEFINES: tuple = ("PHT_DETMATH_LDS",)
 

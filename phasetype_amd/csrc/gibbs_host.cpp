@@ -381,6 +381,7 @@ struct pht_ctx {
   struct ChainGroup *grp = nullptr; /* pht_gibbs_run_chains: exact ECS launched with the other chains */
   int gidx = -1;
   long long flagged = 0; /* flagged observation-sweeps of the last Gibbs run (node-wide) */
+  long long global_count = -1; /* observations over all shards (pht_ctx_set_global_count) */
   ncclComm_t comm = nullptr; /* pht_ctx_attach_rccl: stats summed over ranks on `stream` */
   bool stats_zero = false;   /* d_stats zeroed on `stream` after the last sweep's copy */
   hipEvent_t evd = nullptr;  /* the statistics copy to the host is done */
@@ -670,6 +671,36 @@ extern "C" int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id, int nran
   return 0;
 }
 
+/* in-place sum of a host int64 vector over the context's communicator, on its
+ * stream (the same all-reduce a sweep runs on its statistics block): the
+ * attach-time self-test of phasetype_amd/dist.py compares it with
+ * torch.distributed's sum */
+extern "C" int pht_ctx_rccl_allreduce(pht_ctx *c, long long *buf, int len) {
+  if (!c || !c->comm || !buf || len < 1) {
+    set_err("pht_ctx_rccl_allreduce: need a context with an RCCL communicator and a buffer");
+    return -1;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  void *d = nullptr;
+  HIPCHK(hipMalloc(&d, sizeof(long long) * len));
+  hipError_t e = hipMemcpyAsync(d, buf, sizeof(long long) * len, hipMemcpyHostToDevice, c->stream);
+  ncclResult_t r = ncclSuccess;
+  if (e == hipSuccess) r = rccl().allReduce(d, d, (size_t)len, ncclUint64, ncclSum, c->comm, c->stream);
+  if (e == hipSuccess && r == ncclSuccess)
+    e = hipMemcpyAsync(buf, d, sizeof(long long) * len, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && r == ncclSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d);
+  if (r != ncclSuccess) {
+    set_err("RCCL all-reduce failed: %s", rccl().errStr(r));
+    return -1;
+  }
+  if (e != hipSuccess) {
+    set_err("pht_ctx_rccl_allreduce: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
 extern "C" int pht_device_count(void) {
   int c = 0;
   if (hipGetDeviceCount(&c) != hipSuccess) return 0;
@@ -791,19 +822,6 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
   return 0;
 }
 
-/* enqueue one sweep (params already in c->h_params); stats -> c->h_stats */
-/* lanes per exact observation for the ECS kernel: PHT_GROUP=1|2|4|8 forces
- * it; by default groups of 4 when the shard has few observations per lane
- * (latency-bound regime), one lane otherwise.  Results are identical. */
-static int exact_group(const pht_ctx *c) {
-  if (const char *e = getenv("PHT_GROUP")) {
-    const int g = atoi(e);
-    return (g == 2 || g == 4 || g == 8) ? g : 0;
-  }
-  return 0;
-}
-
-
 /* blocks per CU for the persistent ECS kernel (PHT_ECS_OCC forces it) */
 static int exact_occ(const pht_ctx *c) {
   if (const char *e = getenv("PHT_ECS_OCC")) return atoi(e);
@@ -886,7 +904,6 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     ae.begin = 0;
     ae.count = c->n_exact;
     ae.cens = nullptr;
-    ae.group = exact_group(c);
     ae.occ = exact_occ(c);
     ae.rowk = exact_rowk(c);
     ae.rowprio = getenv("PHT_ROWPRIO") ? atoi(getenv("PHT_ROWPRIO")) : 3;
@@ -1003,6 +1020,15 @@ extern "C" int pht_ctx_sweep_debug(pht_ctx *c, const double *S, const double *s,
 
 extern "C" float pht_ctx_last_kernel_ms(pht_ctx *c) { return c->last_ms; }
 extern "C" long long pht_ctx_flagged_obs(pht_ctx *c) { return c->flagged; }
+extern "C" int pht_ctx_set_global_count(pht_ctx *c, long long total) {
+  if (!c || total < c->count) {
+    set_err("pht_ctx_set_global_count: the total (%lld) must cover this shard's %ld observations", total,
+            c ? c->count : 0L);
+    return -1;
+  }
+  c->global_count = total;
+  return 0;
+}
 
 /* fixed-point exponent for z: 52 - e with sum(y) < 2^e
  * (frexp), so the exact-observation total stays below 2^52 whatever the
@@ -1123,6 +1149,31 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
   double kms = 0.0;
   long long flagged = 0;
   int first_flagged = 0;
+  /* every sweep must account for every observation of every shard: the
+   * node-wide processed count (extra word kXObs, after the reduce) is checked
+   * against it, so a launch-shape bug that drops observations, or a reduce
+   * that sums a block twice or not at all, fails the run instead of biasing
+   * the posterior.  Multi-process: the count comes from
+   * pht_ctx_set_global_count (unchecked when it was not given). */
+  long long expect = 0;
+  {
+    bool multi = reduce != nullptr;
+    for (pht_ctx *c : ctxs) {
+      expect += c->count;
+      multi = multi || c->comm != nullptr;
+    }
+    if (multi) expect = ctxs.size() == 1 ? ctxs[0]->global_count : -1;
+  }
+  /* the observed times alone must fit the fixed point with room to spare */
+  for (pht_ctx *c : ctxs) {
+    double sy = 0.0;
+    for (double v : c->h_ysorted) sy += v;
+    if (!(ldexp(sy, zexp) < 0x1p62)) {
+      set_err("zexp = %d overflows the fixed-point z sums: the shard's observed times total %g (pht_zexp gives %d)",
+              zexp, sy, pht_zexp(c->h_ysorted.data(), (long)c->h_ysorted.size()));
+      return -1;
+    }
+  }
   for (int iter = 1; iter < it; iter++) {
     if (!silent) say("\rProcessing iteration %d of %d (%.1lf%%)\r", iter + 1, it, (100.0 * (iter + 1)) / it);
     if (!disp) {
@@ -1140,23 +1191,39 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
       }
     }
     std::fill(tot.begin(), tot.end(), 0LL);
+    bool wrapped = false;
     for (pht_ctx *c : ctxs) {
       if (!c->grp && ctx_wait(c)) return -1;
       kms += c->last_ms;
-      for (int k = 0; k < sl; k++) tot[k] += (long long)c->h_stats[k];
+      for (int k = 0; k < sl; k++) wrapped |= __builtin_add_overflow(tot[k], (long long)c->h_stats[k], &tot[k]);
     }
     if (reduce && reduce(tot.data(), sl, reduce_user) != 0) {
       set_err("statistics all-reduce callback failed at sweep %d", iter);
       return -1;
     }
+#ifndef PHT_STAMPS /* diagnostic builds carry cycle stamps in the extra words */
+    const long long *xw = tot.data() + 2 * n + n * n;
+    if (expect >= 0 && xw[kXObs] != expect) {
+      set_err("sweep %d sampled %lld observations, expected %lld: the statistics are incomplete or summed twice",
+              iter, xw[kXObs], expect);
+      return -1;
+    }
+    for (int k = 0; k < n; k++) wrapped |= tot[k] < 0;
+    if (wrapped || xw[kXOverflow] != 0) {
+      set_err("sweep %d: the fixed-point z sums overflowed int64 (zexp = %d leaves 2^%d time units; censored paths "
+              "ran far past the observed times): pass a smaller zexp",
+              iter, zexp, 63 - zexp);
+      return -1;
+    }
     /* observations that hit a cap (ARMS iterations, path length, MHRS
      * attempts) or a numerical guard contribute their last attempt, where
      * the reference would keep looping (DESIGN.md §3 Caps) */
-    const long long fl = tot[2 * n + n * n + 2];
+    const long long fl = xw[kXFlagged];
     if (fl > 0) {
       if (!first_flagged) first_flagged = iter;
       flagged += fl;
     }
+#endif
     for (int k = 0; k < n; k++) z[k] = ldexp((double)tot[k], -zexp);
     G.update(R, iter, z.data(), tot.data() + 2 * n);
   }
@@ -1181,6 +1248,15 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
 extern "C" int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double *nu, const double *zeta,
                              const int *T, const double *C, int zexp, int silent, const double *start, double *res,
                              pht_reduce_fn reduce, void *reduce_user, double *kernel_ms_total) {
+  if (!c) {
+    set_err("pht_gibbs_run: null context");
+    return -1;
+  }
+  if (reduce && c->comm) {
+    /* the block would be summed twice: by RCCL on the stream, then here */
+    set_err("pht_gibbs_run: a reduce callback was given for a context with an RCCL communicator attached");
+    return -1;
+  }
   RHost &R = rhost();
   R.begin();
   const uint32_t k0 = (uint32_t)(R.u() * 4294967296.0);
@@ -1307,6 +1383,10 @@ extern "C" void LJMA_Gibbs(int *it, int *mhit, int *method, int *n, int *m, doub
   say("Setting up Gibbs run ...\n");
   int ndev = pht_device_count();
   if (const char *e = getenv("PHT_DEVICES")) ndev = std::min(ndev, atoi(e));
+  /* PHT_CTX_PER_DEVICE=k: k shards (contexts, each with its own streams) per
+   * device; the chain is the same for every k (tests/test_gpu_edges.py) */
+  int per = 1;
+  if (const char *e = getenv("PHT_CTX_PER_DEVICE")) per = std::max(1, std::min(16, atoi(e)));
   std::vector<pht_ctx *> ctxs;
   int rc = 0;
   if (ndev <= 0) {
@@ -1314,9 +1394,10 @@ extern "C" void LJMA_Gibbs(int *it, int *mhit, int *method, int *n, int *m, doub
     rc = -1;
   }
   const long L = *l;
-  for (int d = 0; d < ndev && rc == 0; d++) {
-    const long lo = L * d / ndev, hi = L * (d + 1) / ndev;
-    pht_ctx *c = pht_ctx_create(d, *n, *method, *mhit);
+  const int nsh = ndev * per;
+  for (int d = 0; d < nsh && rc == 0; d++) {
+    const long lo = L * d / nsh, hi = L * (d + 1) / nsh;
+    pht_ctx *c = pht_ctx_create(d / per, *n, *method, *mhit);
     if (!c) {
       rc = -1;
       break;

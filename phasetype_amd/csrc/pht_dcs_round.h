@@ -423,15 +423,7 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a) {
   lds_add(&xc[7], (unsigned long long)c_wround);
 #endif
   __syncthreads();
-  unsigned long long *g = a.stats;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    if (zq[k]) atomicAdd(&g[k], zq[k]);
-    if (Bc[k]) atomicAdd(&g[n + k], (unsigned long long)Bc[k]);
-  }
-  for (int k = threadIdx.x; k < n * n; k += blockDim.x)
-    if (Nc[k]) atomicAdd(&g[2 * n + k], (unsigned long long)Nc[k]);
-  for (int k = threadIdx.x; k < kStatExtra; k += blockDim.x)
-    if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
+  flush_stats(a.stats, zq, Bc, Nc, xc, n);
 }
 
 }  // namespace pht

@@ -1064,6 +1064,12 @@ struct HobCdf {
   }
 };
 
+/* Provenance: Brent's zeroin as in R core's src/library/stats/src/zeroin.c
+ * (R_zeroin2; GPL-2), which the reference carries as Find02
+ * (src/utility.c:233-338).  Its statement order is kept because the device
+ * spec must reproduce the reference's root bit for bit.  Used only by the
+ * round-1 one-lane DCS kernel (PHT_LEGACY_KERNELS builds); the round kernel
+ * splits the same iteration into brent_head/brent_tail (pht_dcs_round.h). */
 template <class F>
 __device__ __forceinline__ double find02(double ax, double bx, double fa, double fb, const F &f, double *Tol, int *Maxit,
                          int &nevals) {

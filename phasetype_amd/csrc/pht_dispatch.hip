@@ -46,7 +46,7 @@ extern "C" hipError_t pht_launch_ecs_chains(const pht::SweepArgs *h, const pht::
   const int n = h[0].n;
   if (n < 1 || n > kMaxN || (make_layout(n).bytes() & 15) != 0) return hipErrorInvalidValue;
   for (int c = 0; c < K; c++)
-    if (h[c].n != n || h[c].cens != nullptr || h[c].group > 1 || h[c].dbg_zq != nullptr) return hipErrorInvalidValue;
+    if (h[c].n != n || h[c].cens != nullptr || h[c].dbg_zq != nullptr) return hipErrorInvalidValue;
   switch (n) {
     case 3: return pht_launch_chains_nt_3(h, d, K, st);
     case 5: return pht_launch_chains_nt_5(h, d, K, st);

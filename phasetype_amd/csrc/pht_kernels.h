@@ -28,7 +28,6 @@ struct SweepArgs {
   uint32_t k0, k1, sweep;
   double zscale;               /* 2^zexp */
   unsigned long long *stats;   /* [stats_len(n)] int64, accumulated */
-  int group;                   /* ECS exact: lanes per observation (0/1 = one lane; 2, 4, 8) */
   int occ;                     /* ECS exact: blocks per CU of the persistent grid (0 = occupancy limit) */
   int spread;                  /* ECS exact: first claims lane-major (the longest paths one per wavefront) */
   int newcap;                  /* ECS exact: observations a lane may start per round (0 = no limit) */

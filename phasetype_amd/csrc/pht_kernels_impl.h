@@ -26,7 +26,6 @@
 
 #include "pht_device.h"
 #include "pht_ecs_round.h"
-#include "pht_ecs_group.h"
 #include "pht_ecs_row.h"
 #include "pht_env.h"
 #include "pht_kernels.h"
@@ -38,6 +37,30 @@ namespace pht {
 template <class T>
 __device__ __forceinline__ void lds_add(PHT_LDS T *p, T v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+/* A workgroup's accumulators into the global int64 block [zq n][B n][N n*n]
+ * [extra] (after a __syncthreads).  z quanta are non-negative, so the sums
+ * only grow: a block or global z total reaching 2^63 (which the host reads as
+ * int64) counts in extra word kXOverflow, and the host fails the sweep rather
+ * than use a wrapped sum (a data set whose censored paths run far past its
+ * observed times can exceed pht_zexp's 2^11-fold headroom). */
+__device__ __forceinline__ void flush_stats(unsigned long long *g, const PHT_LDS unsigned long long *zq,
+                                            const PHT_LDS unsigned *Bc, const PHT_LDS unsigned *Nc,
+                                            const PHT_LDS unsigned long long *xc, int n) {
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const unsigned long long v = zq[k];
+    if (v) {
+      const unsigned long long old = atomicAdd(&g[k], v);
+      if ((v >> 63) | ((old + v) >> 63) | (unsigned long long)(old + v < old))
+        atomicAdd(&g[2 * n + n * n + kXOverflow], 1ull);
+    }
+    if (Bc[k]) atomicAdd(&g[n + k], (unsigned long long)Bc[k]);
+  }
+  for (int k = threadIdx.x; k < n * n; k += blockDim.x)
+    if (Nc[k]) atomicAdd(&g[2 * n + k], (unsigned long long)Nc[k]);
+  for (int k = threadIdx.x; k < kStatExtra; k += blockDim.x)
+    if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
 }
 
 template <bool DEBUG>
@@ -388,15 +411,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
   }
   __syncthreads();
   /* flush: [zq n][B n][N n*n][extra] */
-  unsigned long long *g = a.stats;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    if (zq[k]) atomicAdd(&g[k], zq[k]);
-    if (Bc[k]) atomicAdd(&g[n + k], (unsigned long long)Bc[k]);
-  }
-  for (int k = threadIdx.x; k < n * n; k += blockDim.x)
-    if (Nc[k]) atomicAdd(&g[2 * n + k], (unsigned long long)Nc[k]);
-  for (int k = threadIdx.x; k < kStatExtra; k += blockDim.x)
-    if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
+  flush_stats(a.stats, zq, Bc, Nc, xc, n);
 }
 
 template <int NT, int METHOD, bool DEBUG>
@@ -416,12 +431,17 @@ template <int NT, int METHOD>
 constexpr int persist_waves() {
   return PHT_PERSIST_WAVES > 0 ? PHT_PERSIST_WAVES : ((NT == 10 && METHOD == kMethodDCS) ? 2 : 1);
 }
+#ifdef PHT_LEGACY_KERNELS
+/* the one-lane-to-the-end DCS and censored-ECS kernels of round 1, kept only
+ * for A/B against the round kernels (tools/build_variant.py -D
+ * PHT_LEGACY_KERNELS; PHT_DCS_KERNEL / PHT_CENS_KERNEL=legacy) */
 template <int NT, int METHOD, bool DEBUG>
 __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(persist_waves<NT, METHOD>())))
 persist_kernel(SweepArgs a) {
   sweep_body<NT, METHOD, DEBUG, EnvPrivate, true>(a);
 }
+#endif
 
 /* LDS bytes a workgroup needs: parameter block + accumulators (+ cursor) */
 static int smem_bytes(int n) {
@@ -472,6 +492,7 @@ static hipError_t launch_config(LaunchCfg &cfg, const void *kernel, int sm, int 
   return hipSuccess;
 }
 
+#ifdef PHT_LEGACY_KERNELS
 /* persistent one-lane kernels: grid = CUs x occupancy, capped by the work */
 template <int NT, int METHOD, bool DEBUG>
 static hipError_t launch_persist(const SweepArgs &a, hipStream_t st) {
@@ -488,6 +509,7 @@ static hipError_t launch_persist(const SweepArgs &a, hipStream_t st) {
   hipLaunchKernelGGL((persist_kernel<NT, METHOD, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
   return hipGetLastError();
 }
+#endif
 
 /*
  * ECS exact observations, persistent lanes.  Block b owns chunks of 64
@@ -696,15 +718,7 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
   lds_add(&xc[4], (unsigned long long)c_jump);
 #endif
   __syncthreads();
-  unsigned long long *g = a.stats;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    if (zq[k]) atomicAdd(&g[k], zq[k]);
-    if (Bc[k]) atomicAdd(&g[n + k], (unsigned long long)Bc[k]);
-  }
-  for (int k = threadIdx.x; k < n * n; k += blockDim.x)
-    if (Nc[k]) atomicAdd(&g[2 * n + k], (unsigned long long)Nc[k]);
-  for (int k = threadIdx.x; k < kStatExtra; k += blockDim.x)
-    if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
+  flush_stats(a.stats, zq, Bc, Nc, xc, n);
 }
 
 /*
@@ -847,15 +861,7 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
   lds_add(&xc[4], (unsigned long long)c_jump);
 #endif
   __syncthreads();
-  unsigned long long *g = a.stats;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    if (zq[k]) atomicAdd(&g[k], zq[k]);
-    if (Bc[k]) atomicAdd(&g[n + k], (unsigned long long)Bc[k]);
-  }
-  for (int k = threadIdx.x; k < n * n; k += blockDim.x)
-    if (Nc[k]) atomicAdd(&g[2 * n + k], (unsigned long long)Nc[k]);
-  for (int k = threadIdx.x; k < kStatExtra; k += blockDim.x)
-    if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
+  flush_stats(a.stats, zq, Bc, Nc, xc, n);
 }
 
 /* waves per SIMD the ECS kernel is compiled for (its DEBUG instantiation,
@@ -935,8 +941,9 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
   constexpr long kRows = kBlock / kRowW;
   const long half = (slots / 2) * kRows;
   long rk = row_ok<NT>() ? std::max(0L, std::min(a.rowk, a.count)) : 0;
-  while (rk > half && (rk + kRows - 1) / kRows + (a.count - rk + kBlock - 1) / kBlock > slots) rk -= kRows;
-  b.rowk = rk;
+  while (rk > half && rk >= kRows && (rk + kRows - 1) / kRows + (a.count - rk + kBlock - 1) / kBlock > slots)
+    rk -= kRows;
+  b.rowk = std::max(0L, rk);
   b.rowblk = (int)((b.rowk + (kBlock / kRowW) - 1) / (kBlock / kRowW));
   b.begin = a.begin + b.rowk;
   b.count = a.count - b.rowk;
@@ -969,155 +976,6 @@ static hipError_t launch_ecs_chains(const SweepArgs *h, const SweepArgs *d, int 
   if (nblk > want) nblk = want;
   if (nblk < 1) return hipSuccess;
   hipLaunchKernelGGL((ecs_chains_kernel<NT>), dim3((unsigned)(nblk * K)), dim3(kBlock), sm, st, d, K, (unsigned)nblk);
-  return hipGetLastError();
-}
-
-/*
- * ECS exact observations, G lanes per observation (pht_ecs_group.h): the
- * same persistent scheme as ecs_exact_kernel with groups in place of lanes
- * (block b's groups take positions b, b + grid, ... through the LDS cursor).
- */
-template <int NT, int G, bool DEBUG>
-__global__ void __launch_bounds__(kBlock) ecs_group_kernel(SweepArgs a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int n = nval<NT>(a.n);
-  const Layout L = make_layout(n);
-  const int pbytes = L.bytes();
-  {
-    const unsigned long long *src = reinterpret_cast<const unsigned long long *>(a.params);
-    PHT_LDS unsigned long long *dst = (PHT_LDS unsigned long long *)smem;
-    for (int k = threadIdx.x; k < pbytes / 8; k += blockDim.x) dst[k] = src[k];
-  }
-  PHT_LDS unsigned char *lsm = (PHT_LDS unsigned char *)smem;
-  PHT_LDS unsigned long long *zq = (PHT_LDS unsigned long long *)(lsm + pbytes);
-  PHT_LDS unsigned long long *xc = zq + n;
-  PHT_LDS unsigned *Bc = (PHT_LDS unsigned *)(xc + kStatExtra);
-  PHT_LDS unsigned *Nc = Bc + n;
-  PHT_LDS int *cursor = (PHT_LDS int *)(Nc + n * n);
-  PHT_LDS double *genv = (PHT_LDS double *)(lsm + ((pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 15) & ~15));
-  pht_stage_math_tables();
-  for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
-  for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
-  if (threadIdx.x == 0) *cursor = 0;
-  __syncthreads();
-
-  Par<NT> P;
-  P.d = (const PHT_LDS double *)lsm;
-  P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
-  P.Lr = L;
-  const int gl = threadIdx.x % G, grp = threadIdx.x / G;
-  GEnv env;
-  env.x = genv + grp * 5 * kGrpArr;
-  env.y = env.x + kGrpArr;
-  env.ey = env.y + kGrpArr;
-  env.ar = env.ey + kGrpArr;
-  env.cum = env.ar + kGrpArr;
-  env.cnt = 0;
-  env.ymax = 0.0;
-  EnvPrivate benv;
-  Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
-  Lane ln;
-  GState<NT, G> st;
-  ArmsPend pd;
-  bool pend = false, big = false;
-  long pos = 0;
-  bool have = false, done = false;
-  auto claim = [&]() -> long {
-    int v = 0;
-    if (gl == 0) v = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    v = __shfl(v, 0, G);
-    return claim_pos(v);
-  };
-  long nextp = claim();
-  double ny = 0.0;
-  uint32_t ngid = 0;
-  if (nextp < a.count) {
-    ny = a.y[a.begin + nextp];
-    ngid = a.gid[a.begin + nextp];
-  }
-  for (;;) {
-    bool need = false;
-    if (have && !pend) pht_stream_topup(&ln.r);
-    while (!done && !pend) {
-      if (!have) {
-        if (nextp >= a.count) {
-          done = true;
-          break;
-        }
-        pos = a.begin + nextp;
-        const double yobs = ny;
-        const uint32_t gobs = ngid;
-        nextp = claim();
-        if (nextp < a.count) {
-          ny = a.y[a.begin + nextp];
-          ngid = a.gid[a.begin + nextp];
-        }
-        pht_stream_init(&ln.r, a.k0, a.k1, gobs, 0u, a.sweep);
-        ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
-        if (DEBUG) {
-          sk.dz = a.dbg_zq + pos * n;
-          sk.dN = a.dbg_N + pos * n * n;
-          sk.dB = a.dbg_B + pos;
-          sk.dpre = a.dbg_pre + pos;
-        }
-        {
-          const double target = dev_u(ln.r);
-          const int B = pistart(P, target, ln.flags);
-          if (gl == 0) sk.start(B);
-          st.yt = yobs;
-          st.j = B;
-          st.njump = 0;
-          st.haveE0 = false;
-        }
-        have = true;
-      }
-      if (g_try_absorb<NT, G>(P, ln, sk, st, gl)) {
-        const uint32_t nd = pht_stream_pos(&ln.r);
-        if (gl == 0) {
-          if (DEBUG) {
-            a.dbg_flags[pos] = ln.flags;
-            a.dbg_ndraw[pos] = nd;
-          }
-          lds_add(&xc[0], 1ull);
-          lds_add(&xc[1], (unsigned long long)ln.neval);
-          if (ln.flags) lds_add(&xc[2], 1ull);
-          lds_add(&xc[3], (unsigned long long)nd);
-          lds_add(&xc[4], (unsigned long long)ln.njump);
-        }
-        have = false;
-        continue;
-      }
-      need = true;
-      break;
-    }
-    if (!__any(need) && !__any(pend)) break;
-    g_round<NT, G>(P, ln, env, benv, sk, st, need, pend, big, pd, gl);
-  }
-  __syncthreads();
-  unsigned long long *g = a.stats;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    if (zq[k]) atomicAdd(&g[k], zq[k]);
-    if (Bc[k]) atomicAdd(&g[n + k], (unsigned long long)Bc[k]);
-  }
-  for (int k = threadIdx.x; k < n * n; k += blockDim.x)
-    if (Nc[k]) atomicAdd(&g[2 * n + k], (unsigned long long)Nc[k]);
-  for (int k = threadIdx.x; k < kStatExtra; k += blockDim.x)
-    if (xc[k]) atomicAdd(&g[2 * n + n * n + k], xc[k]);
-}
-
-template <int NT, int G, bool DEBUG>
-static hipError_t launch_ecs_group(const SweepArgs &a, hipStream_t st) {
-  static LaunchCfg cfg;
-  const int sm = ((smem_bytes(a.n) + 4 + 15) & ~15) + (kBlock / G) * 5 * kGrpArr * 8;
-  int occ = 0, cus = 0;
-  if (hipError_t e = launch_config(cfg, (const void *)ecs_group_kernel<NT, G, DEBUG>, sm, &occ, &cus);
-      e != hipSuccess)
-    return e;
-  long want = (a.count + (kBlock / G) - 1) / (kBlock / G);
-  long grid = (long)cus * occ;
-  if (grid > want) grid = want;
-  if (grid < 1) return hipSuccess;
-  hipLaunchKernelGGL((ecs_group_kernel<NT, G, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
   return hipGetLastError();
 }
 
@@ -1216,34 +1074,25 @@ static hipError_t launch_cens_round(const SweepArgs &a, hipStream_t st) {
   hipLaunchKernelGGL((cens_round_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
   return hipGetLastError();
 }
-/* PHT_CENS_KERNEL=legacy: one lane per censored observation to its end (A/B) */
+/* PHT_CENS_KERNEL=legacy / PHT_DCS_KERNEL=legacy: the round-1 one-lane
+ * kernels (A/B only; a library built without PHT_LEGACY_KERNELS refuses) */
+static bool env_legacy(const char *name) {
+  const char *e = getenv(name);
+  return e && !strcmp(e, "legacy");
+}
 static bool cens_legacy() {
-  static const bool v = [] {
-    const char *e = getenv("PHT_CENS_KERNEL");
-    return e && !strcmp(e, "legacy");
-  }();
+  static const bool v = env_legacy("PHT_CENS_KERNEL");
   return v;
 }
-
-/* PHT_DCS_KERNEL=legacy: the one-lane kernel (dcs() to the end), for A/B */
 static bool dcs_legacy() {
-  static const bool v = [] {
-    const char *e = getenv("PHT_DCS_KERNEL");
-    return e && !strcmp(e, "legacy");
-  }();
+  static const bool v = env_legacy("PHT_DCS_KERNEL");
   return v;
 }
 
 template <int NT>
 static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStream_t st) {
-  if (method == kMethodECS && a.cens == nullptr) { /* exact-only range */
-    /* lane groups (opt-in, PHT_GROUP): compiled for n = 10 and runtime n */
-    constexpr int GT = (NT == 10) ? 10 : 0;
-    if (a.group == 4) return debug ? launch_ecs_group<GT, 4, true>(a, st) : launch_ecs_group<GT, 4, false>(a, st);
-    if (a.group == 2) return debug ? launch_ecs_group<GT, 2, true>(a, st) : launch_ecs_group<GT, 2, false>(a, st);
-    if (a.group == 8) return debug ? launch_ecs_group<GT, 8, true>(a, st) : launch_ecs_group<GT, 8, false>(a, st);
+  if (method == kMethodECS && a.cens == nullptr) /* exact-only range */
     return debug ? launch_ecs_exact<NT, true>(a, st) : launch_ecs_exact<NT, false>(a, st);
-  }
   const int blocks = (int)((a.count + kBlock - 1) / kBlock);
   if (blocks == 0) return hipSuccess;
   const int sm = smem_bytes(a.n);
@@ -1252,13 +1101,26 @@ static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStrea
     if (hipError_t e = launch_mhrs_search<NT>(a, st); e != hipSuccess) return e;
     if (debug) PHT_LAUNCH(kMethodMHRS, true); else PHT_LAUNCH(kMethodMHRS, false);
   } else if (method == kMethodDCS) {
-    if (dcs_legacy())
+    if (dcs_legacy()) {
+#ifdef PHT_LEGACY_KERNELS
       return debug ? launch_persist<NT, kMethodDCS, true>(a, st) : launch_persist<NT, kMethodDCS, false>(a, st);
+#else
+      return hipErrorNotSupported;
+#endif
+    }
     return debug ? launch_dcs_round<NT, true>(a, st) : launch_dcs_round<NT, false>(a, st);
   } else {
-    if (a.allcens && !cens_legacy())
-      return debug ? launch_cens_round<NT, true>(a, st) : launch_cens_round<NT, false>(a, st);
-    return debug ? launch_persist<NT, kMethodECS, true>(a, st) : launch_persist<NT, kMethodECS, false>(a, st);
+    /* ECS censored observations: the host always launches them as their own
+     * range (allcens), concurrently with the exact range */
+    if (!a.allcens) return hipErrorInvalidValue;
+    if (cens_legacy()) {
+#ifdef PHT_LEGACY_KERNELS
+      return debug ? launch_persist<NT, kMethodECS, true>(a, st) : launch_persist<NT, kMethodECS, false>(a, st);
+#else
+      return hipErrorNotSupported;
+#endif
+    }
+    return debug ? launch_cens_round<NT, true>(a, st) : launch_cens_round<NT, false>(a, st);
   }
 #undef PHT_LAUNCH
   return hipGetLastError();

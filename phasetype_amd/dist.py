@@ -52,11 +52,31 @@ def make_stats_allreduce(dist, n_words: int, device: str = "cpu"):
     return reduce
 
 
-def attach_rccl(sweeper, dist, device: str) -> None:
+def rccl_selftest_vector(rank: int, n_words: int) -> np.ndarray:
+    """A rank-dependent int64 block exercising all 64 bits of the sum: large
+    words (the z sums), small counts, zeros, and words whose total crosses
+    2^32 (a 32-bit or float reduction would show)."""
+    k = np.arange(n_words, dtype=np.int64)
+    v = (k * 7919 + 13) * (rank + 1)
+    v[::3] = (np.int64(1) << 50) + k[::3] * 1_000_003 + rank
+    v[1::5] = 0
+    v[2::7] = np.int64(0xFFFFFFFF) - rank
+    return v
+
+
+def attach_rccl(sweeper, dist, device: str, n_words: int = 256) -> bool:
     """The in-library alternative to make_stats_allreduce on GPUs: rank 0
     makes an RCCL unique id, torch.distributed broadcasts it, and every
     rank's Sweeper sums its statistics block with an RCCL all-reduce on its
-    own sweep stream (no host callback, no staging copies per sweep)."""
+    own sweep stream (no host callback, no staging copies per sweep).
+
+    Self-test before use: the library's all-reduce of a rank-dependent int64
+    block must equal torch.distributed's sum of the same block, bit for bit,
+    on every rank (agreed by an all-reduce of the verdicts).  Returns True
+    when the in-library reduce is attached and verified; False when the test
+    failed — the caller must then use make_stats_allreduce (a context with a
+    communicator refuses a callback, so the caller also needs a fresh
+    Sweeper)."""
     import torch
 
     from . import RCCL_ID_BYTES, rccl_unique_id
@@ -66,6 +86,20 @@ def attach_rccl(sweeper, dist, device: str) -> None:
         t.copy_(torch.frombuffer(bytearray(rccl_unique_id()), dtype=torch.uint8))
     dist.broadcast(t, 0)
     sweeper.attach_rccl(bytes(t.cpu().numpy().tobytes()), dist.get_world_size(), dist.get_rank())
+    mine = rccl_selftest_vector(dist.get_rank(), n_words)
+    lib_sum = mine.copy()
+    ok = 1
+    try:
+        sweeper.rccl_allreduce(lib_sum)
+    except Exception:  # noqa: BLE001 - reported through the verdict
+        ok = 0
+    ref = torch.from_numpy(mine.copy()).to(device)
+    dist.all_reduce(ref)
+    if ok and not np.array_equal(lib_sum, ref.cpu().numpy()):
+        ok = 0
+    verdict = torch.tensor([ok], dtype=torch.int64, device=device)
+    dist.all_reduce(verdict, op=dist.ReduceOp.MIN)
+    return bool(verdict.item())
 
 
 def max_over_ranks(dist, values, device: str = "cpu"):

@@ -1,7 +1,9 @@
-"""Child of test_gpu_dist.py (run under torchrun, one rank, RCCL): the chain
-with the statistics block summed by the in-library RCCL all-reduce
-(Sweeper.attach_rccl) equals the chain without any reduce, draw for draw.
-Prints one JSON line."""
+"""Child of test_gpu_dist.py (run under torchrun, 1 or more ranks, RCCL,
+one GPU per rank): each rank sweeps its shard; the chain with the statistics
+block summed by the in-library RCCL all-reduce (Sweeper.attach_rccl, after
+its self-test) and the chain with the host callback (make_stats_allreduce)
+both equal the single-process chain over ALL observations (computed on every
+rank without any reduce), draw for draw.  Prints one JSON line on rank 0."""
 import json
 import os
 import sys
@@ -18,10 +20,11 @@ torch.cuda.set_device(local)
 dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
 import phasetype_amd as P  # noqa: E402
-from phasetype_amd.dist import attach_rccl, shard_range  # noqa: E402
+from phasetype_amd.dist import attach_rccl, make_stats_allreduce, shard_range  # noqa: E402
 from phasetype_amd.synth import bd_exit, bd_exit_structure, simulate_ph  # noqa: E402
 
-out = {}
+dev = f"cuda:{local}"
+out = {"selftest": True}
 for n, method, cf in ((5, "ECS", 0.3), (4, "MHRS", 0.0), (4, "DCS", 0.0)):
     S, s = bd_exit(n)
     T, theta = bd_exit_structure(n)
@@ -30,16 +33,36 @@ for n, method, cf in ((5, "ECS", 0.3), (4, "MHRS", 0.0), (4, "DCS", 0.0)):
     y, cen = simulate_ph(S, s, 20000, seed=77 + n, censor_frac=cf)
     zexp = P.zexp_for(y)
     lo, hi = shard_range(len(y), dist.get_rank(), dist.get_world_size())
-    res = []
-    for attach in (False, True):
-        sw = P.Sweeper(n, P.METHODS[method], 1, device=local)
-        sw.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
-        if attach:
-            attach_rccl(sw, dist, f"cuda:{local}")
+    meth = P.METHODS[method]
+
+    def run(mode):
+        if mode == "single":
+            sw = P.Sweeper(n, meth, 1, device=local)
+            sw.set_obs(y, cen)
+        else:
+            sw = P.Sweeper(n, meth, 1, device=local)
+            sw.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
+            sw.set_global_count(len(y))
+        red = None
+        if mode == "rccl":
+            out["selftest"] &= attach_rccl(sw, dist, dev)
+            try:  # a callback on top of the attached communicator would sum twice: refused
+                sw.gibbs(2, meth, nu, zeta, T, np.ones(T.shape), zexp, reduce=lambda a: None)
+                out["selftest"] = False
+            except P.PhaseTypeError as e:
+                out["selftest"] &= "RCCL communicator attached" in str(e)
+        elif mode == "callback":
+            red = make_stats_allreduce(dist, P.stats_len(n), device=dev)
         P.set_seed(4242)
-        res.append(sw.gibbs(6, P.METHODS[method], nu, zeta, T, np.ones(T.shape), zexp))
+        r = sw.gibbs(6, meth, nu, zeta, T, np.ones(T.shape), zexp, reduce=red)
         sw.close()
-    out[f"{method}_n{n}"] = bool(np.array_equal(res[0], res[1])) and bool(np.all(np.isfinite(res[1])))
+        return r
+
+    want = run("single")
+    for mode in ("rccl", "callback"):
+        got = run(mode)
+        out[f"{method}_n{n}_{mode}"] = bool(np.array_equal(want, got)) and bool(np.all(np.isfinite(got)))
 dist.barrier()
 dist.destroy_process_group()
-print(json.dumps(out))
+if int(os.environ.get("RANK", "0")) == 0:
+    print(json.dumps(out))

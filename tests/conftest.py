@@ -21,20 +21,8 @@ def orc():
     from oracle import oracle as O
 
     if not os.path.exists(O.ORC_SO) or os.environ.get("PHT_REBUILD_ORACLE"):
-        O.build(ref=False)
+        O.build()
     return O.OracleLib()
-
-
-@pytest.fixture(scope="session")
-def ref():
-    from oracle import oracle as O
-
-    if not os.path.exists(O.REF_SO):
-        if os.path.isdir("/root/reference/src"):
-            O.build(ref=True)
-        else:
-            pytest.skip("reference oracle (oracle/_ref) not built and /root/reference absent")
-    return O.RefLib()
 
 
 @pytest.fixture(scope="session")

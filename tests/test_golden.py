@@ -1,11 +1,12 @@
-"""CPU: the oracle pinned against the reference.
+"""CPU: the restatement against its committed regression vectors.
 
-tests/golden/*.npz were produced by the reference's own C (oracle/_ref, built
-from /root/reference/src, see tools/make_golden.py).  Bar: the restatement's
-"ref" variant (R stream + libm) reproduces them bit for bit.  Where
-oracle/_ref is present, the reference is re-run as well, so the fixtures
-themselves are re-validated and the restatement is also checked on fresh
-random cases (tests/test_oracle_ref.py).
+tests/golden/g1-g3 hold whole chains and per-observation sweeps of the
+restatement's "ref" variant (R stream + libm + the reference's arithmetic
+order; tools/make_golden.py).  They were first written in round 1 by a build
+of the reference against stand-in R headers, which the rules class as
+unbuildable; round 3 regenerated them from the restatement, bit
+for bit.  So they are regression vectors, not pins: parity with the reference
+is unpinned.  Bar: the "ref" variant reproduces them bit for bit.
 """
 import os
 
@@ -60,24 +61,3 @@ def test_g3_per_observation_restatement(orc, n, method, mhit):
     assert np.array_equal(o["N"], d[k + "_N"].astype(np.int32))
     # G4: the RNG consumption of every observation (MT words drawn)
     assert np.array_equal(o["nword"], d[k + "_nw"])
-
-
-@pytest.mark.parametrize("n,method,mhit", G3[:4] + G3[8:])
-def test_g3_reference_reproduces_fixture(ref, n, method, mhit):
-    d = _load("g3_sweeps")
-    k = f"n{n}_m{method}_h{mhit}"
-    ref.set_seed(int(d[k + "_seed"]))
-    nw = np.zeros(len(d[f"n{n}_y"]), np.uint32)
-    B, z, N = ref.sweep(method, d[f"n{n}_S"], d[f"n{n}_s"], d[f"n{n}_y"], d[f"n{n}_cen"], mhit=mhit, nword=nw)
-    assert np.array_equal(B, d[k + "_B"]) and np.array_equal(z, d[k + "_z"])
-    assert np.array_equal(N, d[k + "_N"].astype(np.int32))
-    assert np.array_equal(nw, d[k + "_nw"])
-
-
-def test_g1_reference_reproduces_fixture(ref):
-    d = _load("g1_test_scripts")
-    for tag in ("phtMCMC2", "phtMCMC"):
-        ref.set_seed(int(d[f"{tag}_seed"]))
-        got = ref.gibbs(int(d[f"{tag}_it"]), 1, int(d[f"{tag}_method"]), 3, d[f"{tag}_nu"], d[f"{tag}_zeta"],
-                        d[f"{tag}_T"], np.ones(16), d["x"])
-        assert np.array_equal(got, d[f"{tag}_res"])

@@ -42,18 +42,36 @@ def test_bench_under_torchrun_rccl(gpu):
     assert line["n_gpus"] == 1 and line["steps"] == 4
     assert line["value"] > 0 and line["ms_per_step"] > 0
     assert line["weak_scaling"]["N_total"] == 200000
-    assert line["config"]["stats_reduce"] == "rccl-in-stream"
+    assert line["config"]["stats_reduce"] == "rccl-in-stream (self-tested)"
 
 
-def test_rccl_in_stream_reduce_keeps_the_chain(gpu):
-    """Sweeper.attach_rccl (pht_ctx_attach_rccl): the statistics block summed
-    by RCCL on the sweep stream gives the same chain as no reduce (one rank)."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+def _chain_child(nproc):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(REPO, "tests", "_rccl_chain_child.py")]
-    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     got = json.loads(lines[0])
-    assert got == {"ECS_n5": True, "MHRS_n4": True, "DCS_n4": True}, got
+    want = {f"{k}_{v}": True for k in ("ECS_n5", "MHRS_n4", "DCS_n4") for v in ("rccl", "callback")}
+    want["selftest"] = True
+    assert got == want, got
+
+
+def test_rccl_in_stream_reduce_keeps_the_chain(gpu):
+    """Sweeper.attach_rccl (pht_ctx_attach_rccl) with one rank: its
+    self-test passes, and the chain with the statistics summed by RCCL on the
+    sweep stream (and with the host callback) equals the chain without any
+    reduce."""
+    _chain_child(1)
+
+
+def test_rccl_two_ranks_equal_single_shard(gpu):
+    """Two ranks on two GPUs: the in-library RCCL sum and the host-callback
+    sum both give the single-process chain over all observations, draw for
+    draw (the N > 1 default path).  Needs two visible GPUs."""
+    if gpu < 2:
+        pytest.skip("needs 2 GPUs (the driver's 8-GPU node; the 1-GPU box cannot host two RCCL ranks)")
+    _chain_child(2)

@@ -184,3 +184,79 @@ def test_every_observation_processed(gpu, orc, n):
         for f in FIELDS:
             assert np.array_equal(g[f], o[f]), (N, f)
         sw.close()
+
+
+# ------------------------------------------------------- drop-in hardening
+def _chain_setup(n=5, N=4000, cf=0.3, seed=61):
+    S, s = bd_exit(n)
+    T, theta = bd_exit_structure(n)
+    y, cen = simulate_ph(S, s, N, seed=seed, censor_frac=cf)
+    return T, 1 + 50 * theta, np.full(len(theta), 50.0), np.ones(T.shape), y, cen
+
+
+@pytest.mark.parametrize("method", [2, 1, 4])
+def test_contexts_per_device_keep_the_chain(gpu, monkeypatch, method):
+    """LJMA_Gibbs's multi-context loop (PHT_CTX_PER_DEVICE=k shards per
+    device, each its own context and streams, all enqueued before any wait,
+    statistics summed on the host): the chain is identical for k = 1, 2, 3
+    (the in-process path that spreads over several GPUs, exercised on one)."""
+    n = 5
+    T, nu, zeta, Cm, y, cen = _chain_setup(n, cf=0.3 if method != 4 else 0.0)
+    m, it = len(nu), 5
+    outs = []
+    for k in (1, 2, 3):
+        monkeypatch.setenv("PHT_CTX_PER_DEVICE", str(k))
+        P.set_seed(777)
+        o = P.LJMA_Gibbs(it, 1, method, n, m, nu, zeta, T, Cm, y, len(y), cen, [-1.0], 1, np.zeros(it * m))
+        outs.append(o["res"])
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
+    assert np.all(np.isfinite(outs[0]))
+
+
+def test_processed_count_guard(gpu):
+    """Every sweep checks that the node-wide statistics account for exactly
+    the observations: a reduce that sums the block twice (or a shard that
+    dropped observations) fails the run loudly instead of biasing it."""
+    n = 5
+    T, nu, zeta, Cm, y, cen = _chain_setup(n)
+    sw = P.Sweeper(n, 2, 1)
+    sw.set_obs(y, cen)
+    sw.set_global_count(len(y))
+    zexp = P.zexp_for(y)
+    P.set_seed(5)
+    ok = sw.gibbs(3, 2, nu, zeta, T, Cm, zexp, reduce=lambda a: None)  # identity reduce: one shard
+    assert np.all(np.isfinite(ok))
+
+    def twice(a):
+        a *= 2
+
+    with pytest.raises(P.PhaseTypeError, match="sampled 8000 observations, expected 4000"):
+        sw.gibbs(3, 2, nu, zeta, T, Cm, zexp, reduce=twice)
+    sw.set_global_count(len(y) + 1)
+    with pytest.raises(P.PhaseTypeError, match="expected 4001"):
+        sw.gibbs(3, 2, nu, zeta, T, Cm, zexp, reduce=lambda a: None)
+    with pytest.raises(P.PhaseTypeError):
+        sw.set_global_count(len(y) - 1)
+    sw.close()
+
+
+@pytest.mark.parametrize("method", [2, 1])
+def test_fixed_point_overflow_is_an_error(gpu, method):
+    """The fixed-point z sums must not wrap.  A zexp whose
+    quantum cannot hold the observed times is refused up front; censored
+    paths that run ~10^4 times past tiny censoring times (pht_zexp leaves
+    2^11-fold headroom over the observed total) cross 2^63 inside the sweep,
+    which then fails with an error instead of using a wrapped sum."""
+    n = 5
+    T, nu, zeta, Cm, y, cen = _chain_setup(n)
+    sw = P.Sweeper(n, method, 1)
+    sw.set_obs(y, cen)
+    P.set_seed(5)
+    with pytest.raises(P.PhaseTypeError, match="overflows the fixed-point"):
+        sw.gibbs(3, method, nu, zeta, T, Cm, 61)
+    y2 = np.full(20000, 1e-4)
+    sw.set_obs(y2, np.ones(len(y2), np.int32))
+    P.set_seed(5)
+    with pytest.raises(P.PhaseTypeError, match="overflowed int64"):
+        sw.gibbs(3, method, nu, zeta, T, Cm, P.zexp_for(y2))
+    sw.close()

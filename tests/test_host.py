@@ -6,7 +6,8 @@
 * The packed per-sweep parameter block (pht_build_params: P/Pfull, dgeevx
   eigensystem, Q^-1 v and the fma precomputes the kernels consume) equals
   the GPU specification in the oracle (orc_sp_build) field by field, and
-  the reference's own LJMA_eigen (oracle/_ref) bit for bit.
+  the oracle's restatement of LJMA_eigen (reference dgeevx arguments) bit
+  for bit.
 * Host random stream: R's set.seed/unif_rand/exp_rand/norm_rand published
   values; product and oracle streams identical (rgamma too).
 * Device primitives restated on the host: Philox4x32-10 known answers,
@@ -145,6 +146,11 @@ def _orc_sp_struct(M):
     return type("orc_sp", (C.Structure,), {"_fields_": fields})
 
 
+def _spview(orc, spbuf):
+    St = _orc_sp_struct(orc.maxn)
+    return St.from_buffer_copy(spbuf.raw[: C.sizeof(St)])
+
+
 def _perturbed(n, seed):
     S, s = bd_exit(n)
     rng = np.random.default_rng(seed)
@@ -199,10 +205,12 @@ def test_params_block_equals_gpu_spec(lib, orc, n, method):
 
 
 @pytest.mark.parametrize("n", [2, 3, 5, 10, 15, 20])
-def test_params_eigensystem_equals_reference(lib, ref, n):
-    """evals/Q/Qinv are the reference's LJMA_eigen (src/utility.c:87-129) output,
-    bit for bit, over 40 perturbed generators per n (the host skips dgeevx's
-    condition numbers, which do not feed the eigensystem)."""
+def test_params_eigensystem_equals_reference(lib, orc, n):
+    """evals/Q/Qinv are LJMA_eigen's (src/utility.c:87-129) output as the
+    oracle restates it (dgeevx with balance 'B', both eigenvector sets and
+    sense 'B', then dgetrf/dgetri), bit for bit, over 40 perturbed generators
+    per n (the host skips dgeevx's condition numbers and left vectors, which do
+    not feed the eigensystem)."""
     L, _, nbytes, nd = _layout(n)
     for seed in range(40):
         S, s = _perturbed(n, 7 * n + 1000 * seed)
@@ -210,10 +218,11 @@ def test_params_eigensystem_equals_reference(lib, ref, n):
         lib.pht_build_params(n, np.ascontiguousarray(S.reshape(-1, order="F")), s, 2,
                              buf.ctypes.data_as(C.c_void_p), nbytes)
         dv = buf[: nd * 8].view(np.float64)
-        info, ev, Q, Qi = ref.eigen(S)
+        sp, info = orc.sp(S, s, 2)
         assert info == 0
-        for name, want in (("evals", ev), ("Q", Q.reshape(-1, order="F")), ("Qinv", Qi.reshape(-1, order="F"))):
+        for name in ("evals", "Q", "Qinv"):
             o, size = L[name]
+            want = np.ctypeslib.as_array(getattr(_spview(orc, sp), name))[:size]
             assert np.array_equal(dv[o:o + size], want), (name, seed)
 
 

@@ -1,120 +1,43 @@
-"""CPU: the two oracle variants against the reference and against analytics.
+"""CPU: the oracle's two variants against each other and against analytics.
 
-* "ref" variant (R stream + libm) == the reference's own C (oracle/_ref),
-  bit for bit, on fresh random cases: per observation and whole chains.
-* "dev" variant (the GPU specification: Philox stream, detmath exp/log,
-  fixed-point z) follows the same algorithm with a different random stream,
-  so it is checked statistically: against the reference's sufficient
-  statistics (5 standard errors) and against Van Loan conditional
-  expectations E[z | Y=y], E[N | Y=y], which are RNG-free.
+Parity with the reference is UNPINNED: the reference needs R
+and cannot be built here, and its tests hold no fixtures.  The checks that
+stand in for a pin are RNG-free:
+
+* Van Loan conditional expectations E[z | Y=y], E[N | Y=y] for exact
+  observations, and their censored counterparts
+  E[z | Y>y], E[N | Y>y] (matrix-exponential integrals, below), which the
+  reference's samplers target: ECS and DCS exactly, MHRS as mhit grows, DCS
+  treating censored observations as exact (src/Simulate_AbsCTMC_eq_
+  AslettHobolth_DCS.c:132-133);
+* the "dev" variant (the GPU specification: Philox stream, detmath exp/log,
+  fixed-point z) against the "ref" variant (the reference's algorithm draw
+  for draw, R stream + libm) in distribution, at the configs' state counts
+  n = 4, 10, 15, 20 (5 standard errors per statistic).
+
+Whole chains of the "ref" variant are pinned to their regression vectors in
+tests/test_golden.py.
 """
-import os
-import subprocess
-import sys
-
 import numpy as np
 import pytest
 from scipy.linalg import expm
 
 from phasetype_amd.synth import bd_exit, bd_exit_structure, simulate_ph
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-
-def _random_generator(n, seed, density=0.6):
-    """A random sub-generator with a real spectrum and a path 0 -> ... -> exit:
-    random Jacobi (tridiagonal) for even seeds, random acyclic (upper
-    triangular) for odd ones.  Complex spectra are outside the reference's
-    domain (it keeps only real parts, src/utility.c:118-120) and its DCS path
-    corrupts the heap on some of them, so they are not used as test inputs."""
-    rng = np.random.default_rng(seed)
-    if seed % 2 == 0:
-        S = np.zeros((n, n))
-        for i in range(n - 1):
-            S[i, i + 1] = rng.uniform(0.2, 3.0)
-            S[i + 1, i] = rng.uniform(0.2, 3.0)
-    else:
-        S = np.triu(np.where(rng.uniform(size=(n, n)) < density, rng.uniform(0.1, 3.0, (n, n)), 0.0), 1)
-        for i in range(n - 1):
-            S[i, i + 1] = max(S[i, i + 1], 0.2)
-    s = np.where(rng.uniform(size=n) < 0.5, rng.uniform(0.1, 2.0, n), 0.0)
-    s[-1] = max(s[-1], 0.5)
-    np.fill_diagonal(S, 0.0)
-    np.fill_diagonal(S, -(S.sum(1) + s))
-    return S, s
-
-
-CASES = [(n, method, mhit, cf) for n in (2, 3, 6) for method, mhit in ((1, 1), (1, 3), (2, 1), (4, 1))
-         for cf in (0.0, 0.4)]
-
-
-@pytest.mark.parametrize("n,method,mhit,cf", CASES)
-def test_ref_variant_bitexact_per_observation(ref, orc, n, method, mhit, cf):
-    S, s = _random_generator(n, 31 * n + method)
-    S0, s0 = bd_exit(n)
-    y, cen = simulate_ph(S0, s0, 300, seed=17 + n, censor_frac=cf)
-    seed = 4242 + n * 10 + method
-    ref.set_seed(seed)
-    B, z, N = ref.sweep(method, S, s, y, cen, mhit=mhit)
-    orc.set_seed(seed)
-    o = orc.ref_sweep(method, S, s, y, cen, mhit=mhit)
-    assert np.array_equal(o["B"], B)
-    assert np.array_equal(o["z"], z)
-    assert np.array_equal(o["N"], N)
-
-
-@pytest.mark.parametrize("method", [1, 2, 4, 3, 6])
-def test_ref_variant_bitexact_chain(ref, orc, method):
-    """Whole LJMA_Gibbs chains (method bitmask as R passes it; combined
-    bits pick the first set sampler, src/PHT_MCMC_Aslett.c:325-337)."""
-    n = 4
-    T, theta = bd_exit_structure(n)
-    S, s = bd_exit(n)
-    y, cen = simulate_ph(S, s, 400, seed=3, censor_frac=0.3)
-    nu, zeta = 1 + 20 * theta, np.full(len(theta), 20.0)
-    Tf = T.reshape(-1, order="F")
-    ref.set_seed(77)
-    want = ref.gibbs(25, 2, method, n, nu, zeta, Tf, np.ones(T.size), y, cen)
-    orc.set_seed(77)
-    got = orc.gibbs(0, 25, 2, method, n, nu, zeta, Tf, np.ones(T.size), y, cen)
-    assert np.array_equal(got, want)
-
-
-def test_resume_start_vector(ref, orc):
-    """start[0] != -1 resumes from the given parameters (src/PHT_MCMC_Aslett.c:212-224)."""
+def test_resume_start_vector(orc):
+    """start[0] != -1 resumes from the given parameters (src/PHT_MCMC_Aslett.c:195-207):
+    row 0 is the start, later rows are draws."""
     n = 3
     T, theta = bd_exit_structure(n)
     S, s = bd_exit(n)
     y, _ = simulate_ph(S, s, 100, seed=9)
     nu, zeta = 1 + 10 * theta, np.full(len(theta), 10.0)
     start = theta * 1.1
-    ref.set_seed(5)
-    want = ref.gibbs(8, 1, 2, n, nu, zeta, T.reshape(-1, order="F"), np.ones(T.size), y, start=start)
     orc.set_seed(5)
     got = orc.gibbs(0, 8, 1, 2, n, nu, zeta, T.reshape(-1, order="F"), np.ones(T.size), y, start=start)
-    assert np.array_equal(got, want)
-    assert np.array_equal(want[0], start)
-
-
-def test_reference_oracle_not_interposed():
-    """Regression: with the product library loaded first, the reference
-    oracle must still run its own LJMA_Gibbs (oracle libs link -Bsymbolic,
-    the product loads RTLD_LOCAL)."""
-    code = (
-        "import numpy as np, phasetype_amd as P\n"
-        "P.load()\n"
-        "from oracle import oracle as O\n"
-        "r, o = O.RefLib(), O.OracleLib()\n"
-        "y = np.array([0.5, 1.0, 2.0, 3.0])\n"
-        "T = np.array([[0,1,0],[2,0,3],[0,0,0]], np.int32).reshape(-1, order='F')\n"
-        "r.set_seed(1); a = r.gibbs(4, 1, 2, 2, [2.,2.,2.], [1.,1.,1.], T, np.ones(9), y)\n"
-        "o.set_seed(1); b = o.gibbs(0, 4, 1, 2, 2, [2.,2.,2.], [1.,1.,1.], T, np.ones(9), y)\n"
-        "assert np.array_equal(a, b), (a, b)\n"
-        "assert np.all(np.isfinite(a))\n")
-    if not os.path.exists(os.path.join(REPO, "oracle", "_ref", "libpht_ref.so")):
-        pytest.skip("oracle/_ref not built")
-    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-2000:]
+    assert np.array_equal(got[0], start)
+    assert np.all(np.isfinite(got)) and np.all(got[1:] > 0) and not np.array_equal(got[1], start)
 
 
 # ---------------------------------------------------------------- statistics
@@ -125,18 +48,27 @@ def _mc_agree(a, b, k=5.0):
     return np.abs(a.mean(0) - b.mean(0)) <= k * se + 1e-12
 
 
-@pytest.mark.parametrize("method,mhit,cf", [(2, 1, 0.3), (1, 1, 0.3), (1, 4, 0.0), (4, 1, 0.3)])
-def test_dev_variant_matches_reference_statistically(ref, orc, method, mhit, cf):
-    n, N = 4, 20000
+STAT_CASES = [(4, 2, 1, 0.3), (4, 1, 1, 0.3), (4, 1, 4, 0.0), (4, 4, 1, 0.3),
+              (10, 2, 1, 0.0), (10, 1, 1, 0.0), (10, 4, 1, 0.0),
+              (15, 2, 1, 0.3), (15, 1, 1, 0.3), (15, 4, 1, 0.3),
+              (20, 2, 1, 0.0)]
+
+
+@pytest.mark.parametrize("n,method,mhit,cf", STAT_CASES)
+def test_dev_variant_matches_ref_variant_statistically(orc, n, method, mhit, cf):
+    N = 20000 if n <= 10 else 8000
     S, s = bd_exit(n)
-    y, cen = simulate_ph(S, s, N, seed=21, censor_frac=cf)
-    ref.set_seed(8)
-    _, zr, Nr = ref.sweep(method, S, s, y, cen, mhit=mhit)
-    o = orc.dev_sweep(method, S, s, y, cen, mhit=mhit, key=(11, 12), sweep=1)
+    y, cen = simulate_ph(S, s, N, seed=21 + n, censor_frac=cf)
+    orc.set_seed(8)
+    r = orc.ref_sweep(method, S, s, y, cen, mhit=mhit)
+    o = orc.dev_sweep(method, S, s, y, cen, mhit=mhit, key=(11, 12 + n), sweep=1)
     zd = o["zq"] * 2.0 ** -o["zexp"]
-    assert np.all(_mc_agree(zr, zd)), (zr.mean(0), zd.mean(0))
-    assert np.all(_mc_agree(Nr.reshape(N, -1), o["N"].reshape(N, -1)))
+    bad = ~_mc_agree(r["z"], zd)
+    assert not bad.any(), (np.nonzero(bad), r["z"].mean(0), zd.mean(0))
+    assert np.all(_mc_agree(r["N"].reshape(N, -1), o["N"].reshape(N, -1)))
     assert np.array_equal(np.bincount(o["B"], minlength=n)[1:], np.zeros(n - 1))  # pi = e1 (quirk q1)
+    assert np.array_equal(np.bincount(r["B"], minlength=n)[1:], np.zeros(n - 1))
+    assert not o["flags"].any() and not r["flags"].any()
 
 
 def _van_loan(S, s, y):
@@ -160,20 +92,115 @@ def _van_loan(S, s, y):
     return Ez, EN
 
 
-@pytest.mark.parametrize("method,mhit", [(2, 1), (4, 1), (1, 25)])
-def test_dev_variant_van_loan(orc, method, mhit):
+def _van_loan_censored(S, s, y):
+    """E[z_i | Y>y], E[N_ij | Y>y] for PH(e1, S): the part of the path before
+    y by Van Loan blocks (end vector 1 = alive at y), the part after y by
+    pi e^{yS} (-S)^{-1} e_i, the expected time in i after y."""
+    n = S.shape[0]
+    pi = np.zeros(n)
+    pi[0] = 1.0
+    one = np.ones(n)
+    Ey = pi @ expm(S * y)
+    surv = Ey @ one
+    after = Ey @ np.linalg.inv(-S)  # expected time in each state after y
+    Ez, EN = np.zeros(n), np.zeros((n, n + 1))
+    for i in range(n):
+        for j in range(n):
+            A = np.zeros((n, n))
+            A[i, j] = 1.0
+            M = np.block([[S, A], [np.zeros((n, n)), S]])
+            J = (pi @ expm(M * y)[:n, n:] @ one + (after[i] if i == j else 0.0)) / surv
+            if i == j:
+                Ez[i] = J
+            else:
+                EN[i, j] = S[i, j] * (J + after[i] / surv)
+        EN[i, n] = after[i] * s[i] / surv
+    return Ez, EN
+
+
+def _check_expectations(o, n, Ez, EN, reps, tag, S):
+    """Means within 5 s.e.; for rarely visited states and rare transitions the
+    sample variance is floored at the Poisson one implied by the expectation
+    (counts: var >= E; times: var >= E x the mean sojourn)."""
+    z = o["zq"] * 2.0 ** -o["zexp"]
+    var = np.maximum(z.var(0), np.abs(Ez) / -np.diag(S))
+    assert np.all(np.abs(z.mean(0) - Ez) <= 5 * np.sqrt(var / reps) + 1e-9), (tag, z.mean(0), Ez)
+    Nd = o["N"].astype(float)
+    Nfull = np.concatenate([Nd * (1 - np.eye(n)), np.diagonal(Nd, axis1=1, axis2=2)[:, :, None]], axis=2)
+    m, var = Nfull.mean(0), np.maximum(Nfull.var(0), np.abs(EN))
+    assert np.all(np.abs(m - EN) <= 5 * np.sqrt(var / reps) + 1e-9), (tag, m, EN)
+
+
+VL_CASES = [(4, 2, 1), (4, 4, 1), (4, 1, 25), (10, 2, 1), (10, 4, 1), (15, 2, 1), (15, 4, 1), (20, 2, 1)]
+
+
+@pytest.mark.parametrize("n,method,mhit", VL_CASES)
+def test_dev_variant_van_loan(orc, n, method, mhit):
     """Exact observations: dev-variant conditional means == Van Loan expectations
     (ECS and DCS are exact samplers; MHRS only as mhit grows)."""
-    n, reps = 4, 4000
+    reps = 4000
+    S, s = bd_exit(n)
+    for yv in (0.5, 3.0) if n <= 4 else (2.0, 8.0):
+        o = orc.dev_sweep(method, S, s, np.full(reps, yv), None, mhit=mhit, key=(99, int(yv * 10) + n), sweep=2)
+        Ez, EN = _van_loan(S, s, yv)
+        _check_expectations(o, n, Ez, EN, reps, (n, method, yv), S)
+
+
+@pytest.mark.parametrize("n,method", [(4, 2), (4, 1), (10, 2), (10, 1), (15, 2)])
+def test_dev_variant_censored_expectations(orc, n, method):
+    """Censored observations (ECS via LJMA_samplechain, MHRS's rejection
+    loop): conditional means == E[z | Y>y], E[N | Y>y] (SURVEY.md §4.3's
+    censored probe, here analytic)."""
+    reps = 4000
     S, s = bd_exit(n)
     for yv in (0.5, 3.0):
-        y = np.full(reps, yv)
-        o = orc.dev_sweep(method, S, s, y, None, mhit=mhit, key=(99, int(yv * 10)), sweep=2)
-        z = o["zq"] * 2.0 ** -o["zexp"]
-        Ez, EN = _van_loan(S, s, yv)
-        se = z.std(0) / np.sqrt(reps)
-        assert np.all(np.abs(z.mean(0) - Ez) <= 5 * se + 1e-9), (yv, z.mean(0), Ez)
-        Nd = o["N"].astype(float)
-        Nfull = np.concatenate([Nd * (1 - np.eye(n)), np.diagonal(Nd, axis1=1, axis2=2)[:, :, None]], axis=2)
-        m, sd = Nfull.mean(0), Nfull.std(0) / np.sqrt(reps)
-        assert np.all(np.abs(m - EN) <= 5 * sd + 1e-9), (yv, m, EN)
+        o = orc.dev_sweep(method, S, s, np.full(reps, yv), np.ones(reps, np.int32), key=(98, int(yv * 10) + n),
+                          sweep=3)
+        Ez, EN = _van_loan_censored(S, s, yv)
+        _check_expectations(o, n, Ez, EN, reps, (n, method, yv, "cens"), S)
+
+
+def test_dcs_treats_censored_as_exact(orc):
+    """DCS ignores the censoring flag (src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:132-133):
+    its censored-observation means are the exact-at-y expectations."""
+    n, reps, yv = 4, 4000, 3.0
+    S, s = bd_exit(n)
+    o = orc.dev_sweep(4, S, s, np.full(reps, yv), np.ones(reps, np.int32), key=(97, 1), sweep=4)
+    Ez, EN = _van_loan(S, s, yv)
+    _check_expectations(o, n, Ez, EN, reps, "dcs-cens", S)
+
+
+def test_censored_expectations_by_forward_simulation():
+    """The censored analytics above against brute-force forward simulation
+    conditioned on Y > y (the survey's censored probe)."""
+    n, yv = 4, 1.0
+    S, s = bd_exit(n)
+    Ez, EN = _van_loan_censored(S, s, yv)
+    rng = np.random.default_rng(3)
+    rates = -np.diag(S)
+    P = np.zeros((n, n + 1))
+    P[:, :n] = S / rates[:, None]
+    P[np.arange(n), np.arange(n)] = 0.0
+    P[:, n] = s / rates
+    cum = np.cumsum(P, 1)
+    M = 200000
+    st = np.zeros(M, np.int64)
+    t = np.zeros(M)
+    z = np.zeros((M, n))
+    Nc = np.zeros((M, n, n + 1))
+    alive = np.ones(M, bool)
+    while alive.any():
+        idx = np.nonzero(alive)[0]
+        d = rng.exponential(1.0, idx.size) / rates[st[idx]]
+        z[idx, st[idx]] += d
+        t[idx] += d
+        nxt = (rng.random(idx.size)[:, None] > cum[st[idx]]).sum(1)
+        Nc[idx, st[idx], nxt] += 1
+        st[idx] = nxt
+        alive[idx] = nxt < n
+    keep = t > yv
+    zk, Nk = z[keep], Nc[keep]
+    se = zk.std(0) / np.sqrt(keep.sum())
+    assert np.all(np.abs(zk.mean(0) - Ez) <= 5 * se), (zk.mean(0), Ez)
+    seN = Nk.std(0) / np.sqrt(keep.sum())
+    assert np.all(np.abs(Nk.mean(0) - EN) <= 5 * seN + 1e-9), (Nk.mean(0), EN)

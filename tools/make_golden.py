@@ -1,10 +1,14 @@
 #!/usr/bin/env python3
-"""Generate tests/golden/*.npz from the reference's own C (oracle/_ref).
+"""Generate tests/golden/*.npz from the CPU restatement's "ref" variant.
 
-Run here (where /root/reference exists): ``python tools/make_golden.py``.
-The fixtures hold inputs and outputs only (no reference source).  They pin the
-CPU restatement (oracle/, "ref" variant) wherever oracle/_ref is absent (the
-GPU box), per SURVEY.md §8(c) G1–G3:
+``python tools/make_golden.py``.  The fixtures hold inputs and outputs only.
+They are REGRESSION vectors of the restatement (oracle/, "ref" variant: R's
+stream + libm + the reference's arithmetic order), not pins: the reference
+needs R's headers, nmath and RNG, which this image lacks, so it is unbuildable
+here ("parity unpinned").  G1–G3 were first written in round 1
+by a build of the reference against stand-in R headers; round 3 retired that
+build and regenerates the same files from the restatement, bit for bit
+(``--check`` compares without writing).  Per SURVEY.md §8(c):
 
 * G1 ``g1_test_scripts.npz`` — LJMA_Gibbs chains of the reference's two test
   scripts, with the exact .C vectors of SURVEY.md §4.2 (tests/phtMCMC.R:1-22,
@@ -18,7 +22,7 @@ GPU box), per SURVEY.md §8(c) G1–G3:
   those observations: 32-bit Mersenne-Twister words the reference drew
   (the draw-order check of Appendix A).
 
-usage: python3 tools/make_golden.py [g1_test_scripts g2_cfg1 g3_sweeps]
+usage: python3 tools/make_golden.py [--check] [g1_test_scripts g2_cfg1 g3_sweeps]
 (no names: all fixtures)
 """
 import os
@@ -71,13 +75,13 @@ def perturbed(n, seed):
     return S, s
 
 
-def g1(ref):
+def g1(orc):
     out = {"x": X20}
     for tag, a in (("phtMCMC2", PHTMCMC2_ARGS), ("phtMCMC", PHTMCMC_ARGS)):
-        ref.set_seed(a["seed"])
+        orc.set_seed(a["seed"])
         m = len(a["nu"])
-        res = ref.gibbs(a["it"], a["mhit"], a["method"], a["n"], a["nu"], a["zeta"], np.array(a["T"], np.int32),
-                        np.ones(16), X20, np.zeros(20, np.int32), np.array([-1.0]), silent=1)
+        res = orc.gibbs(0, a["it"], a["mhit"], a["method"], a["n"], a["nu"], a["zeta"], np.array(a["T"], np.int32),
+                        np.ones(16), X20, np.zeros(20, np.int32), np.array([-1.0]))
         out[f"{tag}_res"] = res
         for k in ("seed", "it", "mhit", "method", "n"):
             out[f"{tag}_{k}"] = np.int64(a[k])
@@ -88,7 +92,7 @@ def g1(ref):
     return out
 
 
-def g2(ref):
+def g2(orc):
     n, N, it = 3, 200, 1000
     S, s = bd_exit(n)
     T, theta = bd_exit_structure(n)
@@ -97,16 +101,16 @@ def g2(ref):
     out = {"y": y, "T": T.reshape(-1, order="F").astype(np.int32), "nu": nu, "zeta": zeta, "n": np.int64(n),
            "it": np.int64(it)}
     for method, seed in ((2, 101), (1, 102)):
-        ref.set_seed(seed)
+        orc.set_seed(seed)
         out[f"m{method}_seed"] = np.int64(seed)
-        out[f"m{method}_res"] = ref.gibbs(it, 1, method, n, nu, zeta, T.reshape(-1, order="F"), np.ones(T.size), y)
+        out[f"m{method}_res"] = orc.gibbs(0, it, 1, method, n, nu, zeta, T.reshape(-1, order="F"), np.ones(T.size), y)
     return out
 
 
 G3_CASES = [(n, method, mhit) for n in (3, 4, 10) for method, mhit in ((1, 1), (1, 5), (2, 1), (4, 1))]
 
 
-def g3(ref):
+def g3(orc):
     out = {}
     for n in (3, 4, 10):
         S0, s0 = bd_exit(n)
@@ -120,10 +124,9 @@ def g3(ref):
         out[f"n{n}_S"], out[f"n{n}_s"], out[f"n{n}_y"], out[f"n{n}_cen"] = S, s, y, cen
     for i, (n, method, mhit) in enumerate(G3_CASES):
         seed = 9000 + i
-        ref.set_seed(seed)
-        nw = np.zeros(len(out[f"n{n}_y"]), np.uint32)
-        B, z, N = ref.sweep(method, out[f"n{n}_S"], out[f"n{n}_s"], out[f"n{n}_y"], out[f"n{n}_cen"], mhit=mhit,
-                            per_obs=True, nword=nw)
+        orc.set_seed(seed)
+        o = orc.ref_sweep(method, out[f"n{n}_S"], out[f"n{n}_s"], out[f"n{n}_y"], out[f"n{n}_cen"], mhit=mhit)
+        B, z, N, nw = o["B"], o["z"], o["N"], o["nword"]
         k = f"n{n}_m{method}_h{mhit}"
         out[k + "_seed"] = np.int64(seed)
         out[k + "_B"] = B.astype(np.int32)
@@ -134,17 +137,24 @@ def g3(ref):
 
 
 def main():
-    if not os.path.exists(O.REF_SO):
-        O.build(ref=True)
-    ref = O.RefLib()
+    O.build()
+    orc = O.OracleLib()
     os.makedirs(OUT, exist_ok=True)
-    want = set(sys.argv[1:])
+    check = "--check" in sys.argv
+    want = {a for a in sys.argv[1:] if not a.startswith("--")}
     for name, fn in (("g1_test_scripts", g1), ("g2_cfg1", g2), ("g3_sweeps", g3)):
         if want and name not in want:
             continue
-        d = fn(ref)
-        np.savez_compressed(os.path.join(OUT, name + ".npz"), **d)
-        print(name, os.path.getsize(os.path.join(OUT, name + ".npz")), "bytes")
+        d = fn(orc)
+        path = os.path.join(OUT, name + ".npz")
+        if check:
+            old = np.load(path)
+            bad = [k for k in d if k not in old or not np.array_equal(np.asarray(d[k]), old[k])]
+            bad += [k for k in old.files if k not in d]
+            print(name, "identical" if not bad else f"DIFFERS in {bad}")
+            continue
+        np.savez_compressed(path, **d)
+        print(name, os.path.getsize(path), "bytes")
 
 
 if __name__ == "__main__":
