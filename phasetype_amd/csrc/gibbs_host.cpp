@@ -368,6 +368,7 @@ struct pht_ctx {
   unsigned char *h_params = nullptr;     /* pinned */
   std::vector<long> order;               /* sorted position -> local index */
   std::vector<double> h_ysorted;         /* y in device (sorted) order */
+  double ysum = 0.0;                     /* sum of the shard's y (the fixed-point range check) */
   /* debug buffers */
   long long *d_zq = nullptr;
   int *d_N = nullptr, *d_B = nullptr, *d_pre = nullptr, *d_flags = nullptr;
@@ -779,6 +780,10 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
   ctx_free_obs(c);
   ctx_free_dbg(c);
   c->count = count;
+  c->n_exact = 0;
+  c->ysum = 0.0;
+  c->h_ysorted.clear();
+  c->order.clear();
   if (count == 0) return 0;
   std::vector<long> ord(count);
   std::iota(ord.begin(), ord.end(), 0L);
@@ -805,6 +810,8 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
   c->n_exact = 0;
   while (c->n_exact < count && cs[c->n_exact] == 0) c->n_exact++;
   c->h_ysorted = ys;
+  c->ysum = 0.0;
+  for (double v : ys) c->ysum += v;
   c->order = std::move(ord);
   HIPCHK(hipMalloc(&c->d_y, sizeof(double) * count));
   HIPCHK(hipMalloc(&c->d_cens, sizeof(int) * count));
@@ -1166,11 +1173,9 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
   }
   /* the observed times alone must fit the fixed point with room to spare */
   for (pht_ctx *c : ctxs) {
-    double sy = 0.0;
-    for (double v : c->h_ysorted) sy += v;
-    if (!(ldexp(sy, zexp) < 0x1p62)) {
+    if (!(ldexp(c->ysum, zexp) < 0x1p62)) {
       set_err("zexp = %d overflows the fixed-point z sums: the shard's observed times total %g (pht_zexp gives %d)",
-              zexp, sy, pht_zexp(c->h_ysorted.data(), (long)c->h_ysorted.size()));
+              zexp, c->ysum, pht_zexp(c->h_ysorted.data(), (long)c->h_ysorted.size()));
       return -1;
     }
   }

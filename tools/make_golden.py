@@ -22,7 +22,12 @@ build and regenerates the same files from the restatement, bit for bit
   those observations: 32-bit Mersenne-Twister words the reference drew
   (the draw-order check of Appendix A).
 
-usage: python3 tools/make_golden.py [--check] [g1_test_scripts g2_cfg1 g3_sweeps]
+* G5 ``g5_posterior.npz`` — posterior summaries of long "ref"-variant chains
+  (oracle/posterior.py CASES: cfg1 ECS/MHRS, n = 10 ECS, n = 15 with 30 %
+  censoring MHRS/ECS/DCS, n = 20 ECS): per parameter the mean and the
+  5/50/95 % quantiles with batch-means MCSEs.
+
+usage: python3 tools/make_golden.py [--check] [g1_test_scripts g2_cfg1 g3_sweeps g5_posterior]
 (no names: all fixtures)
 """
 import os
@@ -136,13 +141,43 @@ def g3(orc):
     return out
 
 
+def _g5_case(args):
+    name, seed = args
+    from oracle import posterior as PO
+
+    orc = O.OracleLib()
+    n, method, mhit, y, cen, T, nu, zeta = PO.case_inputs(name)
+    it = PO.CASES[name][-1]
+    orc.set_seed(seed)
+    chain = orc.gibbs(0, it + 1, mhit, method, n, nu, zeta, T.reshape(-1, order="F"), np.ones(T.size), y, cen)
+    return name, seed, PO.summarize(chain)
+
+
+def g5(orc):
+    """G5 ``g5_posterior.npz``: posterior summaries (mean, 5/50/95 % quantiles,
+    batch-means MCSE) of "ref"-variant chains for oracle/posterior.py CASES."""
+    import multiprocessing as mp
+
+    from oracle import posterior as PO
+
+    del orc
+    jobs = [(name, 7000 + i) for i, name in enumerate(PO.CASES)]
+    with mp.get_context("fork").Pool(min(len(jobs), 7)) as pool:
+        res = pool.map(_g5_case, jobs)
+    out = {}
+    for name, seed, summ in res:
+        out.update(PO.pack(name, summ))
+        out[f"{name}_seed"] = np.int64(seed)
+    return out
+
+
 def main():
     O.build()
     orc = O.OracleLib()
     os.makedirs(OUT, exist_ok=True)
     check = "--check" in sys.argv
     want = {a for a in sys.argv[1:] if not a.startswith("--")}
-    for name, fn in (("g1_test_scripts", g1), ("g2_cfg1", g2), ("g3_sweeps", g3)):
+    for name, fn in (("g1_test_scripts", g1), ("g2_cfg1", g2), ("g3_sweeps", g3), ("g5_posterior", g5)):
         if want and name not in want:
             continue
         d = fn(orc)
