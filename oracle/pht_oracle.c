@@ -183,7 +183,188 @@ static int dispatch(int method) {
   if (method & ORC_MHRS) return ORC_MHRS;
   if (method & ORC_DCS) return ORC_DCS;
   if (method & ORC_ECS) return ORC_ECS;
+  if (method & ORC_UNIF) return ORC_UNIF;
   return 0;
+}
+
+/* ------------------------------------------------- UNIF (dev variant only)
+ * The uniformisation sampler, restated from its specification in
+ * phasetype_amd/csrc/pht_unif.h (no reference counterpart: an opt-in path
+ * for generators whose spectrum the reference's eigen-based samplers
+ * mishandle, src/utility.c:118-120).  Table layout:
+ * [mu, rinv, K, 0][invk K+1][ax K+1][ac K+1][A (K+1) x n]. */
+#define ORC_UNIF_MAXK 2047
+#define ORC_UNIF_MAXLAM 1300.0
+#define ORC_FLAG_UNIF 64
+
+long orc_unif_tab_doubles(int n, int K) { return 4 + 3L * (K + 1) + (long)(K + 1) * n; }
+
+/* the table length the product picks for a shard with largest time ymax */
+int orc_unif_K(const orc_sp *sp, double ymax) {
+  double mu = 0.0;
+  for (int i = 0; i < sp->n; i++) mu = fmax(mu, -sp->S[i + i * sp->n]);
+  const double lmax = mu * ymax;
+  const double kd = ceil(lmax + 14.0 * sqrt(lmax) + 64.0);
+  return (int)(isfinite(kd) && kd < ORC_UNIF_MAXK ? kd : ORC_UNIF_MAXK);
+}
+
+void orc_unif_table(const orc_sp *sp, int K, double *T) {
+  const int n = sp->n;
+  double mu = 0.0;
+  for (int i = 0; i < n; i++) {
+    const double v = -sp->S[i + i * n];
+    mu = (v > mu) ? v : mu;
+  }
+  const double rinv = 1.0 / mu;
+  T[0] = mu; T[1] = rinv; T[2] = (double)K; T[3] = 0.0;
+  double *invk = T + 4, *ax = invk + (K + 1), *ac = ax + (K + 1), *A = ac + (K + 1);
+  for (int k = 0; k <= K; k++) invk[k] = k ? 1.0 / (double)k : 0.0;
+  for (int j = 0; j < n; j++) A[j] = sp->pi[j];
+  static double Pm[2][ORC_MAXN * ORC_MAXN];
+  for (int j = 0; j < n; j++)
+    for (int c = 0; c < n; c++)
+      Pm[0][c + j * n] = (c == j) ? fma(sp->S[c + c * n], rinv, 1.0) : sp->S[c + j * n] * rinv;
+  int cur = 0;
+  for (int p = 1; p <= K; p <<= 1) {
+    const int rows = (K - p + 1 < p) ? K - p + 1 : p;
+    for (int r = 0; r < rows; r++)
+      for (int j = 0; j < n; j++) {
+        double acc = 0.0;
+        for (int c = 0; c < n; c++) acc = fma(A[(long)r * n + c], Pm[cur][c + j * n], acc);
+        A[(long)(p + r) * n + j] = acc;
+      }
+    if (2 * p <= K)
+      for (int j = 0; j < n; j++)
+        for (int c = 0; c < n; c++) {
+          double acc = 0.0;
+          for (int q = 0; q < n; q++) acc = fma(Pm[cur][c + q * n], Pm[cur][q + j * n], acc);
+          Pm[cur ^ 1][c + j * n] = acc;
+        }
+    cur ^= 1;
+  }
+  for (int k = 0; k <= K; k++) {
+    double sx = 0.0, sc = 0.0;
+    for (int j = 0; j < n; j++) {
+      sx = fma(A[(long)k * n + j], sp->s[j], sx);
+      sc = sc + A[(long)k * n + j];
+    }
+    ax[k] = sx;
+    ac[k] = sc;
+  }
+}
+
+static inline double orc_unif_R(const orc_sp *sp, double rinv, int c, int j) {
+  const int n = sp->n;
+  return (c == j) ? fma(sp->S[c + c * n], rinv, 1.0) : sp->S[c + j * n] * rinv;
+}
+
+static void orc_unif_obs(const orc_sp *sp, const double *T, double y, int cens, pht_stream *r, orc_obs *o,
+                         double zscale, int *neval) {
+  const int n = sp->n;
+  const int K = (int)T[2];
+  const double mu = T[0], rinv = T[1];
+  const double *invk = T + 4, *ax = invk + (K + 1), *ac = ax + (K + 1), *A = ac + (K + 1);
+  orcD_obs_clear(o, n);
+  const double lam = y * mu;
+  const double *a = cens ? ac : ax;
+  int ok = (lam >= 0.0) && (lam <= ORC_UNIF_MAXLAM);
+  int kend = 0;
+  double W = 0.0;
+  if (ok) { /* pass 1: the total weight of (k, j) */
+    double w = 0x1p-1000, wmax = 0.0;
+    int k = 0;
+    for (;;) {
+      W = fma(w, a[k], W);
+      wmax = (w > wmax) ? w : wmax;
+      if (k >= K) { o->flags |= ORC_FLAG_UNIF; break; }
+      if ((double)k >= lam && w < wmax * 0x1p-60) break;
+      k++;
+      w = w * (lam * invk[k]);
+    }
+    kend = k;
+    *neval += k + 1;
+    ok = W > 0.0;
+  }
+  int b = 0, js = 0;
+  if (ok) {
+    const double target = pht_next_u(r) * W;
+    double w = 0x1p-1000, cum = 0.0;
+    int k = 0;
+    for (;;) { /* pass 2: k* */
+      cum = fma(w, a[k], cum);
+      if (cum >= target || k >= kend) break;
+      k++;
+      w = w * (lam * invk[k]);
+    }
+    const int ks = k;
+    const double *Ak = A + (long)ks * n;
+    const double t2 = pht_next_u(r) * a[ks];
+    double c2 = 0.0;
+    js = n - 1;
+    for (int j = 0; j < n; j++) { /* j* */
+      c2 = cens ? c2 + Ak[j] : fma(Ak[j], sp->s[j], c2);
+      if (c2 >= t2) { js = j; break; }
+    }
+    b = js;
+    double tm = y, tend = y;
+    for (int m = ks; m >= 1; m--) { /* the bridge, backward */
+      tm = tm * pht_exp_neg(pht_log(pht_next_u(r)) * invk[m]);
+      const double *Am = A + (long)(m - 1) * n;
+      double tot = 0.0;
+      for (int c = 0; c < n; c++) tot = fma(Am[c], orc_unif_R(sp, rinv, c, b), tot);
+      const double tg = pht_next_u(r) * tot;
+      int cs = b;
+      if (tot > 0.0) {
+        double cum2 = 0.0;
+        for (int c = 0; c < n; c++) {
+          cum2 = fma(Am[c], orc_unif_R(sp, rinv, c, b), cum2);
+          if (cum2 >= tg) { cs = c; break; }
+        }
+      } else {
+        o->flags |= ORC_FLAG_UNIF;
+      }
+      if (cs != b) {
+        orcD_zadd(o, b, tend - tm, zscale);
+        o->N[cs + b * n]++;
+        tend = tm;
+        b = cs;
+      }
+    }
+    orcD_zadd(o, b, tend, zscale);
+  } else {
+    o->flags |= ORC_FLAG_UNIF;
+    js = 0;
+    b = 0;
+    orcD_zadd(o, 0, y, zscale);
+  }
+  o->B = b;
+  if (!cens) {
+    o->N[js + js * n]++;
+    o->pre = js;
+    return;
+  }
+  int j = js; /* censored: on from js at y until absorption */
+  for (int nj = 0;; nj++) {
+    if (nj >= ORC_MAX_JUMPS) { o->flags |= 8; o->N[j + j * n]++; break; }
+    orcD_zadd(o, j, orcD_rexp(r, sp->scale[j]), zscale);
+    const double target = pht_next_u(r);
+    const int cnt = sp->nsuccPf[j];
+    double sofar = 0.0;
+    int sel = -1;
+    for (int q = 0; q < cnt; q++) {
+      const int k = sp->succPf[j * (ORC_MAXN + 1) + q];
+      sofar += sp->Pfull[j + k * n];
+      if (!(sofar < target)) { sel = k; break; }
+    }
+    if (sel < 0) {
+      o->flags |= 1;
+      sel = cnt > 0 ? sp->succPf[j * (ORC_MAXN + 1) + cnt - 1] : n;
+    }
+    if (sel >= n) { o->N[j + j * n]++; break; }
+    o->N[j + sel * n]++;
+    j = sel;
+  }
+  o->pre = j;
 }
 
 /*
@@ -201,6 +382,10 @@ void orc_ref_sweep(const orc_sp *sp, int method, int mhit, const double *y, cons
   int neval = 0, nbrent = 0;
   for (int k = 0; k < n; k++) { z_tot[k] = 0.0; B_tot[k] = 0; }
   for (int k = 0; k < n * n; k++) N_tot[k] = 0;
+  if (m == ORC_UNIF) {
+    fprintf(stderr, "oracle: UNIF has no reference-variant (R stream) counterpart\n");
+    abort();
+  }
   for (long i = 0; i < l; i++) {
     const uint64_t w0 = g_rs.nword;
     if (m == ORC_MHRS) orcR_obs_mhrs(sp, y[i], cens[i], mhit, &g_rs, &o, 0.0);
@@ -231,12 +416,21 @@ void orc_dev_sweep(const orc_sp *sp, int method, int mhit, const double *y, cons
   int m = dispatch(method);
   orc_obs o;
   int neval = 0, nbrent = 0;
+  double *utab = NULL;
+  if (m == ORC_UNIF) {
+    double ymax = 0.0;
+    for (long i = 0; i < l; i++) ymax = fmax(ymax, y[i]);
+    const int K = orc_unif_K(sp, ymax);
+    utab = (double *)malloc(sizeof(double) * orc_unif_tab_doubles(n, K));
+    orc_unif_table(sp, K, utab);
+  }
   for (int k = 0; k < n; k++) { zq_tot[k] = 0; B_tot[k] = 0; }
   for (int k = 0; k < n * n; k++) N_tot[k] = 0;
   for (long i = 0; i < l; i++) {
     pht_stream r;
     pht_stream_init(&r, k0, k1, (uint32_t)(obs0 + i), 0u, sweep);
-    if (m == ORC_MHRS) orcD_obs_mhrs(sp, y[i], cens[i], mhit, &r, &o, zscale);
+    if (m == ORC_UNIF) orc_unif_obs(sp, utab, y[i], cens[i], &r, &o, zscale, &neval);
+    else if (m == ORC_MHRS) orcD_obs_mhrs(sp, y[i], cens[i], mhit, &r, &o, zscale);
     else if (m == ORC_DCS) orcD_obs_dcs(sp, y[i], &r, &o, zscale, &nbrent);
     else if (cens[i]) orcD_obs_censored(sp, y[i], cens[i], &r, &o, zscale, &neval);
     else orcD_obs_ecs_exact(sp, y[i], &r, &o, zscale, &neval);
@@ -246,6 +440,7 @@ void orc_dev_sweep(const orc_sp *sp, int method, int mhit, const double *y, cons
     for (int k = 0; k < n * n; k++) N_tot[k] += o.N[k];
     put_obs(&o, n, i, B, pre, z, zq, N, flags, ndraw);
   }
+  free(utab);
   if (stats) { stats[0] += neval; stats[1] += nbrent; }
 }
 

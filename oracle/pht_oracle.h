@@ -13,6 +13,8 @@
 #define ORC_MHRS 0x1
 #define ORC_ECS 0x2
 #define ORC_DCS 0x4
+/* the opt-in uniformisation sampler (no reference counterpart; dev only) */
+#define ORC_UNIF 0x8
 
 /* per-sweep data handed to the samplers (src/PHT_MCMC_Aslett.c:276-333).
  * All matrices column-major A[i + j*n]; Pfull is n x (n+1). */

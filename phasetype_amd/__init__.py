@@ -26,7 +26,9 @@ from . import build as _build
 
 __all__ = ["load", "LJMA_Gibbs", "phtMCMC", "phtMCMC2", "Sweeper", "gibbs_chains", "PhaseTypeError", "METHODS"]
 
-METHODS = {"MHRS": 1, "ECS": 2, "DCS": 4}  # R/phtMCMC2.R:66-70
+# R/phtMCMC2.R:66-70; "UNIF" (8) is not a reference method: the opt-in
+# uniformisation sampler (phasetype_amd/csrc/pht_unif.h), lowest precedence
+METHODS = {"MHRS": 1, "ECS": 2, "DCS": 4, "UNIF": 8}
 
 
 class PhaseTypeError(RuntimeError):

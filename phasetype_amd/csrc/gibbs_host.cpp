@@ -343,10 +343,13 @@ extern "C" int pht_params_bytes(int n) { return make_layout(n).bytes(); }
 extern "C" int pht_stats_len(int n) { return stats_len(n); }
 
 /* =========================================================== device shard */
+/* the reference's precedence MHRS > DCS > ECS (src/PHT_MCMC_Aslett.c:325-337);
+ * the opt-in uniformisation sampler (no reference counterpart) last */
 static int dispatch_method(int method) {
   if (method & kMethodMHRS) return kMethodMHRS;
   if (method & kMethodDCS) return kMethodDCS;
   if (method & kMethodECS) return kMethodECS;
+  if (method & kMethodUNIF) return kMethodUNIF;
   return 0;
 }
 
@@ -369,6 +372,9 @@ struct pht_ctx {
   std::vector<long> order;               /* sorted position -> local index */
   std::vector<double> h_ysorted;         /* y in device (sorted) order */
   double ysum = 0.0;                     /* sum of the shard's y (the fixed-point range check) */
+  double ymax = 0.0;                     /* largest y of the shard (UNIF table length) */
+  double *d_utab = nullptr;              /* UNIF per-sweep table (pht_unif.h) */
+  long utab_cap = 0;                     /* its capacity in doubles */
   /* debug buffers */
   long long *d_zq = nullptr;
   int *d_N = nullptr, *d_B = nullptr, *d_pre = nullptr, *d_flags = nullptr;
@@ -571,6 +577,9 @@ static void ctx_free_obs(pht_ctx *c) {
   if (c->d_mq0) (void)hipFree(c->d_mq0);
   if (c->d_mq1) (void)hipFree(c->d_mq1);
   if (c->d_mcnt) (void)hipFree(c->d_mcnt);
+  if (c->d_utab) (void)hipFree(c->d_utab);
+  c->d_utab = nullptr;
+  c->utab_cap = 0;
   c->d_y = nullptr; c->d_cens = nullptr; c->d_gid = nullptr;
   c->d_mbest = c->d_mq0 = c->d_mq1 = nullptr;
   c->d_mcnt = nullptr;
@@ -782,6 +791,7 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
   c->count = count;
   c->n_exact = 0;
   c->ysum = 0.0;
+  c->ymax = 0.0;
   c->h_ysorted.clear();
   c->order.clear();
   if (count == 0) return 0;
@@ -811,7 +821,11 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
   while (c->n_exact < count && cs[c->n_exact] == 0) c->n_exact++;
   c->h_ysorted = ys;
   c->ysum = 0.0;
-  for (double v : ys) c->ysum += v;
+  c->ymax = 0.0;
+  for (double v : ys) {
+    c->ysum += v;
+    c->ymax = std::max(c->ymax, v);
+  }
   c->order = std::move(ord);
   HIPCHK(hipMalloc(&c->d_y, sizeof(double) * count));
   HIPCHK(hipMalloc(&c->d_cens, sizeof(int) * count));
@@ -903,6 +917,30 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     a.dbg_pre = c->d_pre;
     a.dbg_flags = c->d_flags;
     a.dbg_ndraw = c->d_ndraw;
+  }
+  if (c->method == kMethodUNIF) {
+    /* table length: the shard's largest lam = mu y with a Poisson margin
+     * (pht_unif.h); observations beyond it are flagged, never wrong */
+    const Layout L = make_layout(c->n);
+    const double *S = reinterpret_cast<const double *>(c->h_params) + L.S;
+    double mu = 0.0;
+    for (int i = 0; i < c->n; i++) mu = std::max(mu, -S[i + i * c->n]);
+    if (!(mu > 0.0) || !std::isfinite(mu)) {
+      set_err("UNIF: the generator's largest exit rate is %g (need a positive finite rate)", mu);
+      return -1;
+    }
+    const double lmax = mu * c->ymax;
+    const double kd = std::ceil(lmax + 14.0 * std::sqrt(lmax) + 64.0);
+    a.uK = (int)std::min<double>(kUnifMaxK, std::isfinite(kd) ? kd : (double)kUnifMaxK);
+    const long need = unif_tab_doubles(c->n, a.uK);
+    if (need > c->utab_cap) {
+      if (c->d_utab) HIPCHK(hipFree(c->d_utab));
+      c->d_utab = nullptr;
+      const long cap = std::max(need, unif_tab_doubles(c->n, std::min(kUnifMaxK, a.uK * 3 / 2)));
+      HIPCHK(hipMalloc(&c->d_utab, sizeof(double) * cap));
+      c->utab_cap = cap;
+    }
+    a.utab = c->d_utab;
   }
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   if (c->method == kMethodECS) {

@@ -14,7 +14,13 @@ constexpr int kBlock = 256;
 constexpr int kMethodMHRS = 0x1;
 constexpr int kMethodECS = 0x2;
 constexpr int kMethodDCS = 0x4;
+/* not a reference method: the uniformisation sampler (pht_unif.h), opt-in */
+constexpr int kMethodUNIF = 0x8;
 constexpr int kMhrsCounters = 16;
+/* UNIF per-sweep table in global memory (pht_unif.h):
+ * [mu, rinv, K, 0][invk K+1][ax K+1][ac K+1][A (K+1) x n] */
+constexpr int kUnifMaxK = 2047; /* last row index (LDS: 3 (K+1) doubles per block) */
+constexpr long unif_tab_doubles(int n, int K) { return 4 + 3L * (K + 1) + (long)(K + 1) * n; }
 
 struct SweepArgs {
   const unsigned char *params; /* packed block (pht_layout.h), device */
@@ -45,6 +51,10 @@ struct SweepArgs {
   uint32_t *mbest;             /* [count * (1 + mhit)] */
   uint32_t *mq0, *mq1;         /* [count * (1 + mhit)] */
   unsigned *mcnt;              /* [kMhrsCounters] */
+  /* UNIF (pht_unif.h): the per-sweep table (written by unif_table_kernel)
+   * and its last row index K */
+  double *utab;
+  int uK;
   /* debug per-observation outputs (DEBUG kernels only) */
   long long *dbg_zq;           /* [count*n] */
   int *dbg_N;                  /* [count*n*n] */

@@ -29,6 +29,7 @@
 #include "pht_ecs_row.h"
 #include "pht_env.h"
 #include "pht_kernels.h"
+#include "pht_unif.h"
 
 namespace pht {
 
@@ -1074,6 +1075,167 @@ static hipError_t launch_cens_round(const SweepArgs &a, hipStream_t st) {
   hipLaunchKernelGGL((cens_round_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
   return hipGetLastError();
 }
+/* ================================================================ UNIF */
+/* The per-sweep uniformisation table (pht_unif.h spec), one workgroup:
+ * mu, R and its squarings in LDS, the forward vectors A_k by doubling
+ * (rows [2^i, 2^(i+1)) from rows [0, 2^i) and P_i), then ax, ac, invk. */
+constexpr int kUnifTabThreads = 1024;
+template <int NT>
+__global__ void __launch_bounds__(kUnifTabThreads) unif_table_kernel(SweepArgs a) {
+  __shared__ double Pm[2][kMaxN * kMaxN];
+  __shared__ double hdr[2];
+  const int n = nval<NT>(a.n);
+  const Layout L = make_layout(n);
+  const double *d = reinterpret_cast<const double *>(a.params);
+  const int K = a.uK;
+  double *T = a.utab;
+  double *invk = T + 4, *ax = invk + (K + 1), *ac = ax + (K + 1), *A = ac + (K + 1);
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (tid == 0) {
+    double mu = 0.0;
+    for (int i = 0; i < n; i++) {
+      const double v = -d[L.S + i + i * n];
+      mu = (v > mu) ? v : mu;
+    }
+    hdr[0] = mu;
+    hdr[1] = 1.0 / mu;
+    T[0] = mu;
+    T[1] = hdr[1];
+    T[2] = (double)K;
+    T[3] = 0.0;
+  }
+  for (int k = tid; k <= K; k += nt) invk[k] = k ? 1.0 / (double)k : 0.0;
+  if (tid < n) A[tid] = d[L.pi + tid];
+  __syncthreads();
+  const double rinv = hdr[1];
+  for (int e = tid; e < n * n; e += nt) { /* Pm[0][c + j n] = R_cj */
+    const int c = e % n, j = e / n;
+    Pm[0][e] = (c == j) ? fma(d[L.S + c + c * n], rinv, 1.0) : d[L.S + c + j * n] * rinv;
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int p = 1; p <= K; p <<= 1) {
+    /* rows p + r, r < p, from rows r and P = Pm[cur] (= R^p) */
+    const int rows = (K - p + 1 < p) ? K - p + 1 : p;
+    for (int e = tid; e < rows * n; e += nt) {
+      const int r = e / n, j = e % n;
+      const double *Ar = A + (long)r * n;
+      double acc = 0.0;
+      for (int c = 0; c < n; c++) acc = fma(Ar[c], Pm[cur][c + j * n], acc);
+      A[(long)(p + r) * n + j] = acc;
+    }
+    if (2 * p <= K) { /* P_{i+1} = P_i P_i */
+      for (int e = tid; e < n * n; e += nt) {
+        const int c = e % n, j = e / n;
+        double acc = 0.0;
+        for (int q = 0; q < n; q++) acc = fma(Pm[cur][c + q * n], Pm[cur][q + j * n], acc);
+        Pm[cur ^ 1][e] = acc;
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  for (int k = tid; k <= K; k += nt) {
+    const double *Ak = A + (long)k * n;
+    double sx = 0.0, sc = 0.0;
+    for (int j = 0; j < n; j++) {
+      sx = fma(Ak[j], d[L.s + j], sx);
+      sc = sc + Ak[j];
+    }
+    ax[k] = sx;
+    ac[k] = sc;
+  }
+}
+
+/* UNIF sweep: persistent lanes, one observation per lane to its end
+ * (claims as the other persistent kernels: 64-position chunks through an
+ * LDS cursor), exact and censored observations in one launch */
+static int smem_bytes_unif(int n, int K) { return ((smem_bytes(n) + 15) & ~15) + 3 * (K + 1) * 8; }
+
+template <int NT, bool DEBUG>
+__global__ void __launch_bounds__(kBlock) unif_kernel(SweepArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int n = nval<NT>(a.n);
+  const Layout L = make_layout(n);
+  const int pbytes = L.bytes();
+  if ((long)blockIdx.x * kClaimChunk >= a.count) return;
+  const Par<NT> P = stage_params<NT>(a, (PHT_LDS unsigned char *)smem);
+  PHT_LDS unsigned char *lsm = (PHT_LDS unsigned char *)smem;
+  PHT_LDS unsigned long long *zq = (PHT_LDS unsigned long long *)(lsm + pbytes);
+  PHT_LDS unsigned long long *xc = zq + n;
+  PHT_LDS unsigned *Bc = (PHT_LDS unsigned *)(xc + kStatExtra);
+  PHT_LDS unsigned *Nc = Bc + n;
+  PHT_LDS int *cursor = (PHT_LDS int *)(Nc + n * n);
+  PHT_LDS double *tl = (PHT_LDS double *)(lsm + ((pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 15) & ~15));
+  const int K = a.uK;
+  const double *T = a.utab;
+  for (int k = threadIdx.x; k < 3 * (K + 1); k += blockDim.x) tl[k] = T[4 + k];
+  for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
+  for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
+  if (threadIdx.x == 0) *cursor = 0;
+  pht_stage_math_tables();
+  __syncthreads();
+  UnifTab U;
+  U.invk = tl;
+  U.ax = tl + (K + 1);
+  U.ac = tl + 2 * (K + 1);
+  U.A = T + 4 + 3 * (K + 1);
+  U.K = K;
+  U.mu = T[0];
+  U.rinv = T[1];
+  Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
+  unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
+  for (;;) {
+    const long p = claim_pos(__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (p >= a.count) break;
+    const long i = a.begin + p;
+    Lane ln;
+    pht_stream_init(&ln.r, a.k0, a.k1, a.gid[i], 0u, a.sweep);
+    ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
+    if (DEBUG) {
+      sk.dz = a.dbg_zq + i * n;
+      sk.dN = a.dbg_N + i * n * n;
+      sk.dB = a.dbg_B + i;
+      sk.dpre = a.dbg_pre + i;
+    }
+    unif_obs<NT>(P, U, a.y[i], a.cens ? a.cens[i] : 0, ln, sk);
+    const uint32_t nd = pht_stream_pos(&ln.r);
+    if (DEBUG) {
+      a.dbg_flags[i] = ln.flags;
+      a.dbg_ndraw[i] = nd;
+    }
+    c_obs++;
+    c_neval += ln.neval;
+    c_flag += ln.flags ? 1u : 0u;
+    c_nd += nd;
+    c_jump += ln.njump;
+  }
+  lds_add(&xc[0], (unsigned long long)c_obs);
+  lds_add(&xc[1], (unsigned long long)c_neval);
+  lds_add(&xc[2], (unsigned long long)c_flag);
+  lds_add(&xc[3], (unsigned long long)c_nd);
+  lds_add(&xc[4], (unsigned long long)c_jump);
+  __syncthreads();
+  flush_stats(a.stats, zq, Bc, Nc, xc, n);
+}
+
+template <int NT, bool DEBUG>
+static hipError_t launch_unif(const SweepArgs &a, hipStream_t st) {
+  if (a.utab == nullptr || a.uK < 1 || a.uK > kUnifMaxK || a.begin != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((unif_table_kernel<NT>), dim3(1), dim3(kUnifTabThreads), 0, st, a);
+  if (a.count < 1) return hipGetLastError();
+  static LaunchCfg cfg;
+  const int sm = smem_bytes_unif(a.n, a.uK);
+  int occ = 0, cus = 0;
+  if (hipError_t e = launch_config(cfg, (const void *)unif_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
+    return e;
+  long grid = (long)cus * occ;
+  const long want = (a.count + kClaimChunk - 1) / kClaimChunk;
+  if (grid > want) grid = want;
+  hipLaunchKernelGGL((unif_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
+  return hipGetLastError();
+}
+
 /* PHT_CENS_KERNEL=legacy / PHT_DCS_KERNEL=legacy: the round-1 one-lane
  * kernels (A/B only; a library built without PHT_LEGACY_KERNELS refuses) */
 static bool env_legacy(const char *name) {
@@ -1093,6 +1255,7 @@ template <int NT>
 static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStream_t st) {
   if (method == kMethodECS && a.cens == nullptr) /* exact-only range */
     return debug ? launch_ecs_exact<NT, true>(a, st) : launch_ecs_exact<NT, false>(a, st);
+  if (method == kMethodUNIF) return debug ? launch_unif<NT, true>(a, st) : launch_unif<NT, false>(a, st);
   const int blocks = (int)((a.count + kBlock - 1) / kBlock);
   if (blocks == 0) return hipSuccess;
   const int sm = smem_bytes(a.n);

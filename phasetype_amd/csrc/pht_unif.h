@@ -1,0 +1,200 @@
+/*
+ * pht_unif.h — the uniformisation sampler ("UNIF", method bit 8): an
+ * opt-in, non-parity path sampler that needs no eigendecomposition, so it
+ * serves generators whose spectrum is complex or defective, where the
+ * reference's ECS/DCS keep only the real parts of the eigenvalues
+ * (src/utility.c:118-120) and are wrong.  It is BASELINE.json cfg3's
+ * "LDS-tiled uniformisation exp{yS}" and north_star's "exp{y_i S} by
+ * uniformisation".  It samples the same conditional path law as ECS (exact
+ * observation: absorbed at y; censored: absorbed after y) exactly, up to a
+ * Poisson tail below 2^-60 of its peak term.  Specification (the oracle's
+ * orc_unif_* in oracle/pht_oracle.c follows it operation for operation):
+ *
+ * Per sweep (unif_table_kernel, one workgroup): mu = max_i -S_ii (i
+ * increasing), rinv = 1 / mu, the uniformised chain R = I + S / mu
+ * (R_cj = S_cj * rinv, R_cc = fma(S_cc, rinv, 1)), its squarings
+ * P_0 = R, P_i = P_{i-1} P_{i-1}, and for k = 0..K the forward vectors
+ * A_k = pi R^k by doubling: A_0 = pi, A_k = A_r P_i with k = 2^i + r,
+ * 0 <= r < 2^i (depth log2 K instead of K); every product sums with fma in
+ * increasing inner index.  ax_k = sum_j A_k[j] s_j (fma, increasing j:
+ * absorption at a virtual step after k steps), ac_k = sum_j A_k[j] (alive),
+ * invk_k = 1 / k.  K covers the shard's largest lam = mu y (host:
+ * mu y_max + 14 sqrt(mu y_max) + 64, at most kUnifMaxK).
+ *
+ * Per observation (unif_obs), lam = y mu, a = ax (exact) or ac (censored):
+ *  1. (k*, j*) ~ Pois(k; lam) A_k[j] (s_j | 1): unnormalised Poisson weights
+ *     w_0 = 2^-1000, w_k = w_{k-1} (lam invk_k); W = sum fma(w_k, a_k, .)
+ *     for k = 0.. until k >= lam and w_k < 2^-60 max w (or k = K: flag);
+ *     k* = first k whose running sum reaches U W (same sums), j* = first j
+ *     whose running sum of A_k*[j] (s_j) reaches U a_k*.  lam > 1300 (where
+ *     the unnormalised weights would overflow) or W = 0: flagged fallback.
+ *  2. The path on [0, y] given X_{k*} = j* is bridged BACKWARD with the
+ *     forward vectors: X_{m-1} ~ A_{m-1}[c] R_{c,X_m} (m = k*, ..., 1), so
+ *     no power table is needed; X_0 ~ pi comes out last (the start state B).
+ *     The k* virtual event times are uniform order statistics on (0, y),
+ *     drawn in decreasing order with the bridge: t_m = t_{m+1} exp(log(U)
+ *     invk_m), t_{k*+1} = y.  Self-loops are virtual; a real transition
+ *     c -> b at t_m closes b's sojourn (z_b += end - t_m) and counts N[c,b].
+ *     Draws per step: U (time), U (state).
+ *  3. Exact: absorbed from j* at y (N[j*,j*]++, the reference's diagonal
+ *     convention).  Censored: from j* at y the chain runs forward
+ *     (memoryless): sojourn Exp(-S_jj) (two words), Pfull categorical over
+ *     succPf (one word; an overrun takes the last candidate, flag 1), until
+ *     absorption.
+ * Draw order: U1 (k*), U2 (j*), [U time, U state] x k*, then the censored
+ * continuation.  Flags: kFlagUnifCap (table end, lam cap, zero weights).
+ */
+#ifndef PHT_UNIF_H
+#define PHT_UNIF_H
+
+#include "pht_device.h"
+
+namespace pht {
+
+constexpr int kFlagUnifCap = 64;      /* UNIF: Poisson table end, lam cap or zero weights */
+constexpr double kUnifMaxLam = 1300.0; /* w_0 = 2^-1000 keeps every weight finite below this */
+/* kUnifMaxK and unif_tab_doubles: pht_kernels.h (the host sizes the table) */
+
+struct UnifTab {
+  const PHT_LDS double *invk, *ax, *ac; /* staged in LDS */
+  const double *A;                      /* global, row k at A + k n */
+  int K;
+  double mu, rinv;
+};
+
+template <int NT>
+__device__ __forceinline__ double unif_R(const Par<NT> &P, double rinv, int c, int j) {
+  return (c == j) ? fma(P.S(c, c), rinv, 1.0) : P.S(c, j) * rinv;
+}
+
+template <int NT, class Sink>
+__device__ __forceinline__ void unif_obs(const Par<NT> &P, const UnifTab &T, double y, int cens, Lane &ln,
+                                         Sink &sk) {
+  const int n = P.n();
+  const double lam = y * T.mu;
+  const PHT_LDS double *a = cens ? T.ac : T.ax;
+  bool ok = (lam >= 0.0) && (lam <= kUnifMaxLam);
+  int kend = 0;
+  double W = 0.0;
+  if (ok) {
+    double w = 0x1p-1000, wmax = 0.0;
+    int k = 0;
+    for (;;) {
+      W = fma(w, a[k], W);
+      wmax = (w > wmax) ? w : wmax;
+      if (k >= T.K) {
+        ln.flags |= kFlagUnifCap;
+        break;
+      }
+      if ((double)k >= lam && w < wmax * 0x1p-60) break;
+      k++;
+      w = w * (lam * T.invk[k]);
+    }
+    kend = k;
+    ln.neval += k + 1;
+    ok = W > 0.0;
+  }
+  int b = 0, js = 0;
+  if (ok) {
+    const double target = dev_u(ln.r) * W;
+    double w = 0x1p-1000, cum = 0.0;
+    int k = 0;
+    for (;;) {
+      cum = fma(w, a[k], cum);
+      if (cum >= target || k >= kend) break;
+      k++;
+      w = w * (lam * T.invk[k]);
+    }
+    const int ks = k;
+    const double *Ak = T.A + (long)ks * n;
+    const double t2 = dev_u(ln.r) * a[ks];
+    double c2 = 0.0;
+    js = n - 1;
+    for (int j = 0; j < n; j++) {
+      c2 = cens ? c2 + Ak[j] : fma(Ak[j], P.s(j), c2);
+      if (c2 >= t2) {
+        js = j;
+        break;
+      }
+    }
+    /* backward bridge */
+    b = js;
+    double tm = y, tend = y;
+    for (int m = ks; m >= 1; m--) {
+      tm = tm * pht_exp_neg(pht_log(dev_u(ln.r)) * T.invk[m]);
+      const double *Am = T.A + (long)(m - 1) * n;
+      double tot = 0.0;
+      for (int c = 0; c < n; c++) tot = fma(Am[c], unif_R(P, T.rinv, c, b), tot);
+      const double tg = dev_u(ln.r) * tot;
+      int cs = b;
+      if (tot > 0.0) {
+        double cum2 = 0.0;
+        for (int c = 0; c < n; c++) {
+          cum2 = fma(Am[c], unif_R(P, T.rinv, c, b), cum2);
+          if (cum2 >= tg) {
+            cs = c;
+            break;
+          }
+        }
+      } else {
+        ln.flags |= kFlagUnifCap;
+      }
+      if (cs != b) {
+        sk.z(b, tend - tm);
+        sk.N(cs, b);
+        ln.njump++;
+        tend = tm;
+        b = cs;
+      }
+    }
+    sk.z(b, tend);
+  } else {
+    ln.flags |= kFlagUnifCap;
+    js = 0;
+    b = 0;
+    sk.z(0, y);
+  }
+  sk.start(b);
+  if (!cens) {
+    sk.N(js, js);
+    sk.pre(js);
+    return;
+  }
+  /* censored: the chain runs on from js at y until absorption */
+  int j = js;
+  for (int nj = 0;; nj++) {
+    if (nj >= kMaxJumps) {
+      ln.flags |= kFlagJumpCap;
+      sk.N(j, j);
+      break;
+    }
+    sk.z(j, dev_rexp(ln.r, P.scale(j)));
+    const double target = dev_u(ln.r);
+    const int cnt = P.nsuccPf(j);
+    double sofar = 0.0;
+    int sel = -1;
+    for (int q = 0; q < cnt; q++) {
+      const int k = P.succPf(j, q);
+      sofar += P.Pf(j, k);
+      if (!(sofar < target)) {
+        sel = k;
+        break;
+      }
+    }
+    if (sel < 0) {
+      ln.flags |= kFlagScanEnd;
+      sel = cnt > 0 ? P.succPf(j, cnt - 1) : n;
+    }
+    if (sel >= n) {
+      sk.N(j, j);
+      break;
+    }
+    sk.N(j, sel);
+    ln.njump++;
+    j = sel;
+  }
+  sk.pre(j);
+}
+
+}  // namespace pht
+#endif

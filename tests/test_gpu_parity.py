@@ -345,3 +345,81 @@ def test_chains_one_launch_ragged(gpu, monkeypatch):
     finally:
         for sw in sws:
             sw.close()
+
+
+# ------------------------------------------- the uniformisation sampler (UNIF)
+def _cyclic(n, seed=0):
+    rng = np.random.default_rng(seed)
+    S = np.zeros((n, n))
+    for i in range(n):
+        S[i, (i + 1) % n] = rng.uniform(1.5, 3.0)
+        S[i, (i - 1) % n] += rng.uniform(0.0, 0.2)
+    s = rng.uniform(0.1, 0.5, n)
+    np.fill_diagonal(S, 0.0)
+    np.fill_diagonal(S, -(S.sum(1) + s))
+    return S, s
+
+
+@pytest.mark.parametrize("n,N,cf,gen", [(3, 3000, 0.3, "bd"), (5, 3000, 0.0, "bd"), (10, 4000, 0.3, "bd"),
+                                        (15, 2000, 0.3, "bd"), (20, 2000, 0.0, "bd"), (7, 2000, 0.3, "bd"),
+                                        (32, 500, 0.3, "bd"), (6, 2000, 0.3, "cyclic"), (12, 2000, 0.0, "cyclic")])
+def test_unif_per_observation_bitexact(gpu, orc, n, N, cf, gen):
+    """UNIF (pht_unif.h: the per-sweep table kernel + the persistent sampler)
+    against the oracle's restatement, per observation: start state, pre-
+    absorption state, flags, draws, fixed-point z and N identical; complex
+    spectra included (cyclic generators)."""
+    S0, s0 = bd_exit(n)
+    y, cen = simulate_ph(S0, s0, N, seed=4000 + n, censor_frac=cf)
+    S, s = _perturbed(n, n + 3) if gen == "bd" else _cyclic(n)
+    key, sweep = (0x51 + n, 0x77), 4
+    zexp = int(orc.lib.orc_zexp(np.ascontiguousarray(y), len(y)))
+    o = orc.dev_sweep(8, S, s, y, cen, key=key, sweep=sweep, zexp=zexp)
+    sw = P.Sweeper(n, 8, 1)
+    sw.set_obs(y, cen)
+    g = sw.sweep_debug(S, s, key=key, sweep=sweep, zexp=zexp)
+    for f in ("B", "pre", "flags", "ndraw"):
+        bad = np.nonzero(g[f] != o[f])[0]
+        assert bad.size == 0, f"{f} differs at obs {bad[:5]}: gpu {g[f][bad[:5]]} oracle {o[f][bad[:5]]}"
+    assert np.array_equal(g["zq"], o["zq"]) and np.array_equal(g["N"], o["N"])
+    st = sw.sweep(S, s, key=key, sweep=sweep, zexp=zexp)
+    assert np.array_equal(st[:2 * n + n * n], g["stats"][:2 * n + n * n])
+    assert P.split_stats(st, n)[3][0] == N
+    assert not o["flags"].any()
+
+
+def test_unif_chain_bitexact(gpu, orc):
+    """pht_gibbs_run and LJMA_Gibbs with method 8 == the oracle's UNIF chain."""
+    n = 6
+    T, theta = bd_exit_structure(n)
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 3000, seed=8, censor_frac=0.3)
+    m, it = len(theta), 10
+    nu, zeta = 1 + 50 * theta, np.full(m, 50.0)
+    Cm = np.ones_like(T, dtype=np.float64)
+    orc.set_seed(99)
+    want = orc.gibbs(1, it, 1, 8, n, nu, zeta, T.reshape(-1, order="F"), Cm.reshape(-1, order="F"), y, cen)
+    P.set_seed(99)
+    sw = P.Sweeper(n, 8, 1)
+    sw.set_obs(y, cen)
+    assert np.array_equal(sw.gibbs(it, 8, nu, zeta, T, Cm, P.zexp_for(y)), want)
+    P.set_seed(99)
+    out = P.LJMA_Gibbs(it, 1, 8, n, m, nu, zeta, T, Cm, y, len(y), cen, [-1.0], 1, np.zeros(it * m))
+    assert np.array_equal(out["res"].reshape(m, it).T, want)
+
+
+def test_unif_shard_invariance(gpu):
+    n, N = 10, 6000
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, N, seed=91, censor_frac=0.3)
+    zexp = P.zexp_for(y)
+    full = P.Sweeper(n, 8)
+    full.set_obs(y, cen)
+    a = full.sweep(S, s, key=(5, 6), sweep=3, zexp=zexp)
+    k = 2 * n + n * n
+    tot = np.zeros(k, dtype=a.dtype)
+    for lo, hi in ((0, 17), (17, 2500), (2500, N)):
+        sw = P.Sweeper(n, 8)
+        sw.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
+        tot += sw.sweep(S, s, key=(5, 6), sweep=3, zexp=zexp)[:k]
+        sw.close()
+    assert np.array_equal(a[:k], tot)

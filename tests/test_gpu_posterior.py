@@ -58,6 +58,24 @@ def test_ljma_gibbs_chain_matches_reference_posterior(gpu, name):
     assert ok, (name, worst, bad[:5])
 
 
+@pytest.mark.parametrize("name", ["cfg1_ecs", "n10_ecs", "n15_cens_ecs", "n20_ecs"])
+def test_unif_chain_matches_ecs_reference_posterior(gpu, name):
+    """The uniformisation sampler (method 8, no reference counterpart)
+    samples the same conditional path law as ECS, so its chain must match the
+    reference ECS posterior of the same data within the same tolerance."""
+    n, method, mhit, y, cen, T, nu, zeta = PO.case_inputs(name)
+    assert method == 2
+    ref = PO.unpack(np.load(GOLD), name)
+    sw = P.Sweeper(n, 8, 1)
+    sw.set_obs(y, cen)
+    P.set_seed(2718)
+    chain = sw.gibbs(GPU_SWEEPS + 1, 8, nu, zeta, T, np.ones(T.shape), P.zexp_for(y))
+    sw.close()
+    ok, worst, bad = PO.compare(PO.summarize(chain), ref)
+    assert ok, (name, worst, bad[:5])
+    assert sw.flagged_obs == 0
+
+
 def test_gpu_chain_detects_shifted_data(gpu):
     """Power of the same comparison: data scaled by 1.1 must fail it."""
     n, method, mhit, y, cen, T, nu, zeta = PO.case_inputs("n10_ecs")

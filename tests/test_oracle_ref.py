@@ -204,3 +204,58 @@ def test_censored_expectations_by_forward_simulation():
     assert np.all(np.abs(zk.mean(0) - Ez) <= 5 * se), (zk.mean(0), Ez)
     seN = Nk.std(0) / np.sqrt(keep.sum())
     assert np.all(np.abs(Nk.mean(0) - EN) <= 5 * seN + 1e-9), (Nk.mean(0), EN)
+
+
+# ------------------------------------------- the uniformisation sampler (UNIF)
+def _cyclic(n, seed=0):
+    """A generator with a complex spectrum: a cycle 0 -> 1 -> ... -> n-1 -> 0
+    with exits and weak back-steps (the reference's ECS/DCS keep only the real
+    parts of its eigenvalues, src/utility.c:118-120)."""
+    rng = np.random.default_rng(seed)
+    S = np.zeros((n, n))
+    for i in range(n):
+        S[i, (i + 1) % n] = rng.uniform(1.5, 3.0)
+        S[i, (i - 1) % n] += rng.uniform(0.0, 0.2)
+    s = rng.uniform(0.1, 0.5, n)
+    np.fill_diagonal(S, 0.0)
+    np.fill_diagonal(S, -(S.sum(1) + s))
+    return S, s
+
+
+@pytest.mark.parametrize("n,gen", [(4, "bd"), (10, "bd"), (20, "bd"), (5, "cyclic"), (12, "cyclic")])
+def test_unif_van_loan(orc, n, gen):
+    """UNIF (method 8, the uniformisation sampler of pht_unif.h) is an exact
+    sampler of the conditional path law: its conditional means equal the
+    Van Loan expectations for exact AND censored observations, also for
+    generators with complex spectra (where eigen-based samplers fail)."""
+    S, s = bd_exit(n) if gen == "bd" else _cyclic(n)
+    if gen == "cyclic":
+        assert np.abs(np.linalg.eigvals(S).imag).max() > 0.1  # really complex
+    reps = 4000
+    for yv in (0.5, 3.0, 8.0):
+        for cens in (0, 1):
+            o = orc.dev_sweep(8, S, s, np.full(reps, yv), np.full(reps, cens, np.int32), key=(7, n), sweep=9)
+            assert not o["flags"].any()
+            Ez, EN = (_van_loan_censored if cens else _van_loan)(S, s, yv)
+            _check_expectations(o, n, Ez, EN, reps, (n, gen, yv, cens), S)
+
+
+def test_unif_shard_and_order_invariance(orc):
+    """An observation's UNIF result depends only on its own id, y and the
+    parameters: a shard (obs0 offset, a different table length K from its
+    own largest y) reproduces the full run's per-observation results."""
+    n = 6
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 3000, seed=5, censor_frac=0.3)
+    full = orc.dev_sweep(8, S, s, y, cen, key=(1, 2), sweep=3, zexp=40)
+    part = orc.dev_sweep(8, S, s, y[1000:1100], cen[1000:1100], key=(1, 2), sweep=3, zexp=40, obs0=1000)
+    for f in ("B", "pre", "zq", "N", "ndraw"):
+        assert np.array_equal(full[f][1000:1100], part[f]), f
+
+
+def test_unif_flags_extreme_lam(orc):
+    """mu y beyond 1300 (the unnormalised Poisson weights would overflow) is
+    a flagged cap, not a wrong draw."""
+    S, s = bd_exit(3)
+    o = orc.dev_sweep(8, S, s, np.array([1.0, 600.0]), np.zeros(2, np.int32), key=(1, 1), sweep=1, zexp=30)
+    assert o["flags"][0] == 0 and o["flags"][1] & 64
