@@ -82,10 +82,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", "--states", dest="n", type=int, default=10)
     ap.add_argument("--N", "--obs", dest="N", type=int, default=1_000_000)
-    ap.add_argument("--method", default="ECS", choices=["ECS", "MHRS", "DCS"])
+    ap.add_argument("--method", default="ECS", choices=["ECS", "MHRS", "DCS", "UNIF"])
     ap.add_argument("--censor", type=float, default=0.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling side measurement (N > 1)")
+    ap.add_argument("--no-alt", action="store_true", help="skip the UNIF side measurement")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_latest.json"))
     args = ap.parse_args()
 
@@ -176,6 +177,43 @@ def main():
         raise SystemExit("non-finite Gibbs draws")
     sw.close()
 
+    # Side measurement (not `value`): the same workload through the opt-in
+    # uniformisation sampler (method 8, pht_unif.h), which samples the same
+    # conditional path law as ECS exactly and is posterior-tested against
+    # the reference's ECS chains (tests/test_gpu_posterior.py).  `value`
+    # stays the reference's own sampler.
+    alt = None
+    if args.method == "ECS" and not args.no_alt:
+        sw3 = P.Sweeper(n, P.METHODS["UNIF"], 1, device=local)
+        sw3.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
+        sw3.set_global_count(N)
+        red3 = None
+        if dist is not None:
+            if in_lib:
+                if not attach_rccl(sw3, dist, coll_dev):
+                    raise SystemExit("in-library RCCL all-reduce passed its self-test once, then failed it")
+            else:
+                red3 = make_stats_allreduce(dist, P.stats_len(n), device=coll_dev)
+        P.set_seed(20241010)
+        w3 = sw3.gibbs(args.warmup + 1, P.METHODS["UNIF"], nu, zeta, T, Cm, zexp, reduce=red3)
+        sync()
+        t3 = time.perf_counter()
+        r3 = sw3.gibbs(args.steps + 1, P.METHODS["UNIF"], nu, zeta, T, Cm, zexp, start=w3[-1], reduce=red3)
+        sync()
+        dt3 = time.perf_counter() - t3
+        k3 = sw3.kernel_ms_total / args.steps
+        if dist is not None:
+            dt3, k3 = max_over_ranks(dist, [dt3, k3], device=coll_dev)
+        if not np.all(np.isfinite(r3)) or sw3.flagged_obs:
+            raise SystemExit("UNIF side run: non-finite draws or flagged observations")
+        sw3.close()
+        alt = {"method": "UNIF", "value": args.steps / dt3, "unit": "iterations/s", "ms_per_step": dt3 / args.steps * 1e3,
+               "kernel_ms": k3, "note": "side measurement, same workload and timing as `value`: the opt-in "
+                                        "uniformisation sampler (method 8; per-sweep table kernel + sampler "
+                                        "kernel), an exact sampler of ECS's conditional path law with no "
+                                        "eigendecomposition; posterior-tested against the reference's ECS "
+                                        "chains. `value` is the reference's default ECS sampler"}
+
     weak = None
     if dist is not None and not args.no_weak:
         # Side measurement (not `value`): weak scaling, every rank holding N
@@ -248,11 +286,16 @@ def main():
                                      "unit": "TFLOP/s", "frac": tfs / FP64_VALU_PEAK_TF,
                                      "note": "FP64 lane-flops per launch from PMC (SQ_INSTS_VALU_FLOPS_FP64 x 64 x "
                                              "VALU lane utilisation, profiles/traffic_latest.json) / kernel time"}
+        if alt is not None:
+            line["alt_sampler"] = alt
         if weak is not None:
             line["weak_scaling"] = weak
         if world == 1 and not args.no_cpu_baseline:
+            # UNIF has no reference counterpart: its CPU baseline is the
+            # reference's own sampler for the same workload, ECS
+            cpu_method = method if method in (1, 2, 4) else 2
             try:
-                line["cpu_baseline"] = cpu_baseline(n, y, cen, T, nu, zeta, method)
+                line["cpu_baseline"] = cpu_baseline(n, y, cen, T, nu, zeta, cpu_method)
             except Exception as e:  # noqa: BLE001
                 log(f"[bench] cpu baseline failed: {e}")
                 line["cpu_baseline"] = None
@@ -262,7 +305,7 @@ def main():
                 import subprocess
 
                 cmd = [sys.executable, "-m", "oracle.cpu_best", "--n", str(n), "--N", str(N), "--censor",
-                       str(args.censor), "--workers", "16", "--seconds", "10", "--method", str(method)]
+                       str(args.censor), "--workers", "16", "--seconds", "10", "--method", str(cpu_method)]
                 out = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=180, check=True).stdout
                 line["cpu_best"] = json.loads(out.strip().splitlines()[-1])
                 line["cpu_best"]["ratio_gpu_over_cpu_best"] = line["value"] / line["cpu_best"]["value"]

@@ -105,6 +105,20 @@ int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id128, int nranks, int 
  * exposed so the caller can check it against its own collective. */
 int pht_ctx_rccl_allreduce(pht_ctx *c, long long *buf, int len);
 
+/* Device-resident Gibbs chain (opt-in, NON-PARITY):
+ * the conjugate Gamma update (src/PHT_MCMC_Aslett.c:340-397) and the next
+ * sweep's parameter block (:279-297) run on the device between sweeps
+ * (phasetype_amd/csrc/pht_resident.hip), so the host enqueues every sweep
+ * and waits once.  Gamma draws come from a counter-based sampler
+ * (include/pht_gamma.h), not R's rgamma: the chain is deterministic under
+ * set.seed but not the host loop's chain.  Eigen-free samplers only (method
+ * 8 UNIF or 1 MHRS, matching the context's method); an attached RCCL
+ * communicator sums every sweep's statistics on the stream (every rank must
+ * use the same R-stream seed).  Arguments and res layout as pht_gibbs_run;
+ * kernel_ms_total = device time of all sweeps. */
+int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, const double *nu, const double *zeta, const int *T,
+                           const double *C, int zexp, const double *start, double *res, double *kernel_ms_total);
+
 /* Independent chains at once (no reference counterpart —
  * the reference runs one chain per LJMA_Gibbs call, src/PHT_MCMC_Aslett.c:104):
  * chain c on ctxs[c] (one context each, same n/method/mhit, observations set),

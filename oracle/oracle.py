@@ -118,6 +118,7 @@ class OracleLib:
         L.orc_zexp.argtypes = [_dp, C.c_long]
         L.orc_gibbs.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _dp,
                                 _dp, C.c_long, _ip, _dp, _dp]
+        L.orc_rgamma_ctr_v.argtypes = [C.c_uint32, C.c_uint32, C.c_double, C.c_double, C.c_long, _dp]
 
     def set_seed(self, seed: int) -> None:
         self.lib.orc_set_seed(seed & 0xFFFFFFFF)
@@ -174,7 +175,16 @@ class OracleLib:
                        N=N.reshape(l, n, n).transpose(0, 2, 1), flags=fl, ndraw=nd)
         return out
 
+    def rgamma_ctr(self, a, scale, cnt, key=(1, 2)):
+        """cnt draws of the device-resident chain's Gamma sampler (include/pht_gamma.h)."""
+        out = np.zeros(cnt)
+        self.lib.orc_rgamma_ctr_v(key[0], key[1], a, scale, cnt, out)
+        return out
+
     def gibbs(self, dev, it, mhit, method, n, nu, zeta, T, C_, y, censored=None, start=None):
+        """dev: 0 the reference's algorithm (R stream), 1 the GPU spec (host
+        Gamma update: pht_gibbs_run), 2 the device-resident chain
+        (pht_gibbs_run_resident: counter-based Gamma draws)."""
         if censored is None:
             censored = np.zeros(len(y), np.int32)
         if start is None:

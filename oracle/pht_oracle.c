@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include "pht_detmath.h"
+#include "pht_gamma.h"
 #include "pht_philox.h"
 #include "../phasetype_amd/csrc/rstream.h"
 #include "pht_oracle.h"
@@ -461,10 +462,12 @@ typedef struct { int i, j; double c; } ent;
 
 /*
  * LJMA_Gibbs restated (src/PHT_MCMC_Aslett.c:104-410).  dev=0: the sampler
- * step is orc_ref_sweep on the global R stream (bit-exact with the
- * reference).  dev=1: the sampler step is orc_dev_sweep, keyed by two
+ * step is orc_ref_sweep on the global R stream (the reference's algorithm
+ * draw for draw).  dev=1: the sampler step is orc_dev_sweep, keyed by two
  * uniforms drawn from the R stream at entry (k = floor(u * 2^32)), exactly
- * as the product's LJMA_Gibbs does.  The linked-list parameter maps are kept
+ * as the product's LJMA_Gibbs does.  dev=2: as dev=1 with the conjugate
+ * draws from the counter-based Gamma sampler (include/pht_gamma.h): the
+ * product's device-resident chain (pht_gibbs_run_resident).  The linked-list parameter maps are kept
  * as arrays visited in the lists' (reverse-insertion) order, which fixes the
  * floating summation order of zsum and of the diagonal refresh.
  */
@@ -495,8 +498,17 @@ void orc_gibbs(int dev, int it, int mhit, int method, int n, int m, const double
   for (int i = 0; i < n1; i++) Dl[i] = malloc((size_t)n1 * sizeof(ent));
 
   if (start[0] < 0) {
-    for (int i = 0; i < m; i++)
-      res[0 + (size_t)i * it] = (nu[i] > 1) ? (nu[i] - 1.0) / zeta[i] : pht_rs_rgamma(&g_rs, nu[i], 1.0 / zeta[i]);
+    for (int i = 0; i < m; i++) {
+      if (nu[i] > 1) {
+        res[0 + (size_t)i * it] = (nu[i] - 1.0) / zeta[i];
+      } else if (dev == 2) {
+        pht_stream gs;
+        pht_stream_init(&gs, k0, k1, PHT_GAMMA_OBS(i), PHT_GAMMA_TAG, 0u);
+        res[0 + (size_t)i * it] = pht_rgamma_ctr(&gs, nu[i], 1.0 / zeta[i]);
+      } else {
+        res[0 + (size_t)i * it] = pht_rs_rgamma(&g_rs, nu[i], 1.0 / zeta[i]);
+      }
+    }
   } else {
     for (int i = 0; i < m; i++) res[0 + (size_t)i * it] = start[i];
   }
@@ -551,7 +563,15 @@ void orc_gibbs(int dev, int it, int mhit, int method, int n, int m, const double
       for (int e = nz[k] - 1; e >= 0; e--) zsum[k] += z[zl[k][e].i] / zl[k][e].c;
     }
     for (int k = 0; k < m; k++) {
-      double tmp = res[iter + (size_t)k * it] = pht_rs_rgamma(&g_rs, nu[k] + Nsum[k], 1.0 / (zeta[k] + zsum[k]));
+      double draw;
+      if (dev == 2) {
+        pht_stream gs;
+        pht_stream_init(&gs, k0, k1, PHT_GAMMA_OBS(k), PHT_GAMMA_TAG, (uint32_t)iter);
+        draw = pht_rgamma_ctr(&gs, nu[k] + Nsum[k], 1.0 / (zeta[k] + zsum[k]));
+      } else {
+        draw = pht_rs_rgamma(&g_rs, nu[k] + Nsum[k], 1.0 / (zeta[k] + zsum[k]));
+      }
+      double tmp = res[iter + (size_t)k * it] = draw;
       for (int e = nTT[k] - 1; e >= 0; e--) TT[TTl[k][e].i + TTl[k][e].j * n1] = tmp * TTl[k][e].c;
       for (int e = nS[k] - 1; e >= 0; e--) S[Sl[k][e].i + Sl[k][e].j * n] = tmp * Sl[k][e].c;
       for (int e = ns[k] - 1; e >= 0; e--) s[sl[k][e].i] = tmp * sl[k][e].c;
@@ -582,4 +602,14 @@ void orc_stream_u(uint32_t k0, uint32_t k1, uint32_t obs, uint32_t tag, uint32_t
   pht_stream s;
   pht_stream_init(&s, k0, k1, obs, tag, sweep);
   for (long i = 0; i < cnt; i++) out[i] = pht_next_u(&s);
+}
+
+/* probe for tests: n Gamma(a, scale) draws from the counter streams
+ * (key k0,k1; parameter index i, sweep i) */
+void orc_rgamma_ctr_v(uint32_t k0, uint32_t k1, double a, double scale, long cnt, double *out) {
+  for (long i = 0; i < cnt; i++) {
+    pht_stream s;
+    pht_stream_init(&s, k0, k1, PHT_GAMMA_OBS(i & 1023), PHT_GAMMA_TAG, (uint32_t)(i >> 10));
+    out[i] = pht_rgamma_ctr(&s, a, scale);
+  }
 }

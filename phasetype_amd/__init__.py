@@ -49,6 +49,7 @@ EXPORTS = [
     "pht_unif_rand", "pht_rgamma", "pht_in_R", "pht_set_verbose", "pht_zexp", "pht_params_bytes", "pht_stats_len",
     "pht_build_params", "pht_ctx_create", "pht_ctx_destroy", "pht_ctx_set_obs", "pht_ctx_sweep",
     "pht_ctx_sweep_debug", "pht_ctx_last_kernel_ms", "pht_ctx_flagged_obs", "pht_ctx_set_global_count", "pht_gibbs_run",
+    "pht_gibbs_run_resident",
     "pht_gibbs_run_chains", "pht_rccl_unique_id", "pht_ctx_attach_rccl", "pht_ctx_rccl_allreduce",
 ]
 
@@ -101,6 +102,8 @@ def load(build_if_needed: bool = True) -> C.CDLL:
     L.pht_ctx_set_global_count.argtypes = [C.c_void_p, C.c_longlong]
     L.pht_gibbs_run.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _dp, C.c_int, C.c_int,
                                 _dp, _dp, C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]
+    L.pht_gibbs_run_resident.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _dp, C.c_int, _dp,
+                                         _dp, C.POINTER(C.c_double)]
     L.pht_gibbs_run_chains.argtypes = [C.POINTER(C.c_void_p), C.c_int, _up, C.c_int, C.c_int, C.c_int, _dp, _dp,
                                        _ip, _dp, C.c_int, _dp, _dp, C.POINTER(C.c_double)]
     L.pht_rccl_unique_id.argtypes = [C.c_void_p]
@@ -249,6 +252,24 @@ class Sweeper:
                                   np.ascontiguousarray(zeta, np.float64), Tf, Cf, zexp, int(silent), start, res,
                                   C.cast(cb, C.c_void_p) if cb else None, None, C.byref(kms))
         if rc != 0:
+            raise _err(self.L)
+        self.kernel_ms_total = kms.value
+        self.flagged_obs = int(self.L.pht_ctx_flagged_obs(self.ctx))
+        return res.reshape(m, it).T.copy()
+
+    def gibbs_resident(self, it, method, nu, zeta, T, C_, zexp, start=None):
+        """The device-resident chain (pht_gibbs_run_resident; opt-in,
+        non-parity: Gamma draws from the device's counter-based sampler):
+        every sweep and conjugate update runs on the GPU, one host wait."""
+        m = len(nu)
+        res = np.zeros(it * m, np.float64)
+        start = np.array([-1.0]) if start is None else np.ascontiguousarray(start, np.float64)
+        kms = C.c_double(0.0)
+        Tf = np.ascontiguousarray(np.asarray(T).reshape(-1, order="F"), np.int32)
+        Cf = np.ascontiguousarray(np.asarray(C_, np.float64).reshape(-1, order="F"))
+        if self.L.pht_gibbs_run_resident(self.ctx, it, method, m, np.ascontiguousarray(nu, np.float64),
+                                         np.ascontiguousarray(zeta, np.float64), Tf, Cf, zexp, start, res,
+                                         C.byref(kms)) != 0:
             raise _err(self.L)
         self.kernel_ms_total = kms.value
         self.flagged_obs = int(self.L.pht_ctx_flagged_obs(self.ctx))

@@ -22,10 +22,10 @@ LIB = os.path.join(OUT_DIR, "libPhaseType.so")
 KERNEL_NTS = (10, 3, 5, 15, 20, 0)  # compile-time n of the kernels (0 = runtime n)
 # (source, extra defines) per object
 UNITS = [("pht_kernels_nt.hip", (f"PHT_NT={k}",)) for k in KERNEL_NTS] + [
-    ("pht_dispatch.hip", ()), ("gibbs_host.cpp", ()), ("rstream.c", ())]
+    ("pht_dispatch.hip", ()), ("pht_resident.hip", ()), ("gibbs_host.cpp", ()), ("rstream.c", ())]
 SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = ["pht_device.h", "pht_env.h", "pht_kernels.h", "pht_kernels_impl.h", "pht_layout.h", "rstream.h",
-           "pht_ecs_round.h", "pht_ecs_row.h", "pht_dcs_round.h", "pht_cens_round.h"]
+           "pht_ecs_round.h", "pht_ecs_row.h", "pht_dcs_round.h", "pht_cens_round.h", "pht_unif.h"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 DEFAULT_DEFINES: tuple = ("PHT_DETMATH_LDS",)
 
@@ -42,7 +42,8 @@ def needs_build() -> bool:
         return True
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps += [os.path.join(REPO, "include", f) for f in ("phasetype_amd.h", "pht_detmath.h", "pht_philox.h")]
+    deps += [os.path.join(REPO, "include", f) for f in ("phasetype_amd.h", "pht_detmath.h", "pht_philox.h",
+                                                          "pht_gamma.h")]
     deps.append(__file__)
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 

@@ -932,6 +932,7 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     const double lmax = mu * c->ymax;
     const double kd = std::ceil(lmax + 14.0 * std::sqrt(lmax) + 64.0);
     a.uK = (int)std::min<double>(kUnifMaxK, std::isfinite(kd) ? kd : (double)kUnifMaxK);
+    a.uymax = c->ymax;
     const long need = unif_tab_doubles(c->n, a.uK);
     if (need > c->utab_cap) {
       if (c->d_utab) HIPCHK(hipFree(c->d_utab));
@@ -1403,6 +1404,230 @@ extern "C" int pht_gibbs_run_chains(pht_ctx **ctxs, int nchains, const uint32_t 
     mx = std::max(mx, kms[c]);
   }
   if (kernel_ms_max) *kernel_ms_max = mx;
+  return 0;
+}
+
+/* ============================================ device-resident Gibbs chain */
+/*
+ * pht_gibbs_run_resident (opt-in, NON-PARITY): the whole
+ * Gibbs loop on the device.  Per sweep the stream carries the step-1 kernels,
+ * the optional RCCL all-reduce of the statistics, and resident_update_kernel
+ * (pht_resident.hip: conjugate Gamma update by a counter-based sampler, the
+ * next sweep's parameter block, the per-sweep checks); the host enqueues all
+ * sweeps and waits once.  Eigen-free samplers only (UNIF, MHRS): ECS/DCS need
+ * the host's LAPACK eigensystem every sweep.  The chain is a deterministic
+ * function of the R stream's two key words (drawn at entry, as
+ * pht_gibbs_run does) but NOT the host loop's chain (R's rgamma is replaced).
+ */
+namespace {
+struct DevBuf {
+  void *p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+}  // namespace
+
+extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, const double *nu, const double *zeta,
+                                      const int *T, const double *C, int zexp, const double *start, double *res,
+                                      double *kernel_ms_total) {
+  if (!c || it < 1 || m < 1 || m > (kMaxN + 1) * (kMaxN + 1)) {
+    set_err("pht_gibbs_run_resident: need a context, it >= 1 and 1 <= m <= (kMaxN+1)^2");
+    return -1;
+  }
+  const int disp = dispatch_method(method);
+  if ((disp != kMethodUNIF && disp != kMethodMHRS) || disp != c->method) {
+    set_err("pht_gibbs_run_resident: the resident chain runs the eigen-free samplers UNIF (8) or MHRS (1), on a "
+            "context created for that method (got method %d, context %d)", method, c->method);
+    return -1;
+  }
+  if (!(ldexp(c->ysum, zexp) < 0x1p62)) {
+    set_err("zexp = %d overflows the fixed-point z sums (the shard's observed times total %g)", zexp, c->ysum);
+    return -1;
+  }
+  const int n = c->n, n1 = n + 1;
+  RHost &R = rhost();
+  R.begin();
+  const uint32_t k0 = (uint32_t)(R.u() * 4294967296.0);
+  const uint32_t k1 = (uint32_t)(R.u() * 4294967296.0);
+  R.end();
+  /* GibbsState's parameter lists as CSR, insertion order */
+  std::vector<std::vector<int>> nl(m), zi(m), tl(m), dl(n1);
+  std::vector<std::vector<double>> zc(m), tc(m);
+  for (int i = 0; i < n1; i++)
+    for (int j = 0; j < n1; j++) {
+      const int t = T[i + j * n1];
+      if (t == 0) continue;
+      if (t < 1 || t > m) {
+        set_err("pht_gibbs_run_resident: T[%d,%d] = %d outside 0..m", i, j, t);
+        return -1;
+      }
+      const int k = t - 1;
+      const double cc = C[i + j * n1];
+      nl[k].push_back(j == n ? i + i * n : i + j * n);
+      zi[k].push_back(i);
+      zc[k].push_back(cc);
+      tl[k].push_back(i + j * n1);
+      tc[k].push_back(cc);
+      dl[i].push_back(i + j * n1);
+    }
+  std::vector<int> ints;   /* nl_off[m+1] nl_idx zl_off[m+1] zl_i tl_off[m+1] tl_ij dl_off[n+1] dl_ij */
+  std::vector<double> dbl; /* nu[m] zeta[m] start[m] zl_c tl_c */
+  auto csr = [&](const std::vector<std::vector<int>> &v, int rows, int &off, int &idx) {
+    off = (int)ints.size();
+    int acc = 0;
+    for (int r = 0; r < rows; r++) {
+      ints.push_back(acc);
+      acc += (int)v[r].size();
+    }
+    ints.push_back(acc);
+    idx = (int)ints.size();
+    for (int r = 0; r < rows; r++) ints.insert(ints.end(), v[r].begin(), v[r].end());
+  };
+  int o_nl, i_nl, o_zl, i_zl, o_tl, i_tl, o_dl, i_dl;
+  csr(nl, m, o_nl, i_nl);
+  csr(zi, m, o_zl, i_zl);
+  csr(tl, m, o_tl, i_tl);
+  csr(dl, n, o_dl, i_dl);
+  dbl.insert(dbl.end(), nu, nu + m);
+  dbl.insert(dbl.end(), zeta, zeta + m);
+  const bool has_start = start && start[0] >= 0;
+  for (int k = 0; k < m; k++) dbl.push_back(has_start ? start[k] : 0.0);
+  const int o_zc = (int)dbl.size();
+  for (int k = 0; k < m; k++) dbl.insert(dbl.end(), zc[k].begin(), zc[k].end());
+  const int o_tc = (int)dbl.size();
+  for (int k = 0; k < m; k++) dbl.insert(dbl.end(), tc[k].begin(), tc[k].end());
+
+  HIPCHK(hipSetDevice(c->device));
+  DevBuf bi, bd, bres, btt, bfl, berr;
+  HIPCHK(hipMalloc(&bi.p, sizeof(int) * ints.size()));
+  HIPCHK(hipMalloc(&bd.p, sizeof(double) * dbl.size()));
+  HIPCHK(hipMalloc(&bres.p, sizeof(double) * (size_t)it * m));
+  HIPCHK(hipMalloc(&btt.p, sizeof(double) * n1 * n1));
+  HIPCHK(hipMalloc(&bfl.p, sizeof(unsigned long long)));
+  HIPCHK(hipMalloc(&berr.p, sizeof(int)));
+  hipStream_t st = c->stream;
+  HIPCHK(hipMemcpyAsync(bi.p, ints.data(), sizeof(int) * ints.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(bd.p, dbl.data(), sizeof(double) * dbl.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(btt.p, 0, sizeof(double) * n1 * n1, st));
+  HIPCHK(hipMemsetAsync(bfl.p, 0, sizeof(unsigned long long), st));
+  HIPCHK(hipMemsetAsync(berr.p, 0, sizeof(int), st));
+  HIPCHK(hipMemsetAsync(c->d_params, 0, make_layout(n).bytes(), st));
+  HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * stats_len(n), st));
+  c->stats_zero = false;
+  const int *di = static_cast<const int *>(bi.p);
+  const double *dd = static_cast<const double *>(bd.p);
+  ResidentArgs ra;
+  memset(&ra, 0, sizeof ra);
+  ra.n = n;
+  ra.m = m;
+  ra.it = it;
+  ra.init = 1;
+  ra.zs = ldexp(1.0, -zexp);
+  ra.expect = c->global_count >= 0 ? c->global_count : (c->comm ? -1 : (long long)c->count);
+  ra.k0 = k0;
+  ra.k1 = k1;
+  ra.nu = dd;
+  ra.zeta = dd + m;
+  ra.start = has_start ? dd + 2 * m : nullptr;
+  ra.nl_off = di + o_nl;
+  ra.nl_idx = di + i_nl;
+  ra.zl_off = di + o_zl;
+  ra.zl_i = di + i_zl;
+  ra.zl_c = dd + o_zc;
+  ra.tl_off = di + o_tl;
+  ra.tl_ij = di + i_tl;
+  ra.tl_c = dd + o_tc;
+  ra.dl_off = di + o_dl;
+  ra.dl_ij = di + i_dl;
+  ra.stats = c->d_stats;
+  ra.TT = static_cast<double *>(btt.p);
+  ra.res = static_cast<double *>(bres.p);
+  ra.params = c->d_params;
+  ra.flagged = static_cast<unsigned long long *>(bfl.p);
+  ra.err = static_cast<int *>(berr.p);
+  HIPCHK(pht_launch_resident_update(&ra, 0, st));
+  ra.init = 0;
+
+  SweepArgs a;
+  memset(&a, 0, sizeof a);
+  a.params = c->d_params;
+  a.n = n;
+  a.mhit = c->mhit;
+  a.count = c->count;
+  a.y = c->d_y;
+  a.cens = c->d_cens;
+  a.gid = c->d_gid;
+  a.k0 = k0;
+  a.k1 = k1;
+  a.zscale = ldexp(1.0, zexp);
+  a.stats = c->d_stats;
+  a.mbest = c->d_mbest;
+  a.mq0 = c->d_mq0;
+  a.mq1 = c->d_mq1;
+  a.mcnt = c->d_mcnt;
+  if (disp == kMethodUNIF) {
+    /* table capacity: twice the prior mode's largest exit rate (the device
+     * sizes each sweep's table from its own mu within it; rows beyond flag) */
+    double mu0 = 0.0;
+    {
+      std::vector<double> rowsum(n1, 0.0);
+      for (int i = 0; i < n1; i++)
+        for (int j = 0; j < n1; j++) {
+          const int t = T[i + j * n1];
+          if (t == 0) continue;
+          const int k = t - 1;
+          const double th = has_start ? start[k] : (nu[k] > 1 ? (nu[k] - 1.0) / zeta[k] : nu[k] / zeta[k]);
+          rowsum[i] += th * C[i + j * n1];
+        }
+      for (int i = 0; i < n; i++) mu0 = std::max(mu0, rowsum[i]);
+    }
+    const double lmax = 2.0 * mu0 * c->ymax;
+    const double kd = std::ceil(lmax + 14.0 * std::sqrt(lmax) + 64.0);
+    a.uK = (int)std::min<double>(kUnifMaxK, std::isfinite(kd) ? kd : (double)kUnifMaxK);
+    a.uymax = c->ymax;
+    const long need = unif_tab_doubles(n, a.uK);
+    if (need > c->utab_cap) {
+      if (c->d_utab) HIPCHK(hipFree(c->d_utab));
+      c->d_utab = nullptr;
+      HIPCHK(hipMalloc(&c->d_utab, sizeof(double) * need));
+      c->utab_cap = need;
+    }
+    a.utab = c->d_utab;
+  }
+  HIPCHK(hipEventRecord(c->ev0, st));
+  for (int iter = 1; iter < it; iter++) {
+    a.sweep = (uint32_t)iter;
+    if (c->count > 0 || disp == kMethodUNIF) HIPCHK(pht_launch_sweep(&a, disp, 0, st));
+    if (c->comm) {
+      const ncclResult_t rr =
+          rccl().allReduce(c->d_stats, c->d_stats, (size_t)stats_len(n), ncclUint64, ncclSum, c->comm, st);
+      if (rr != ncclSuccess) {
+        set_err("RCCL all-reduce of the statistics failed: %s", rccl().errStr(rr));
+        return -1;
+      }
+    }
+    HIPCHK(pht_launch_resident_update(&ra, iter, st));
+  }
+  HIPCHK(hipEventRecord(c->ev1, st));
+  unsigned long long fl = 0;
+  int err = 0;
+  HIPCHK(hipMemcpyAsync(res, bres.p, sizeof(double) * (size_t)it * m, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&fl, bfl.p, sizeof fl, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&err, berr.p, sizeof err, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  if (kernel_ms_total) *kernel_ms_total = ms;
+  c->flagged = (long long)fl;
+  if (err) {
+    set_err("resident chain: %s%s%s", (err & 1) ? "a sweep did not sample every observation; " : "",
+            (err & 2) ? "the fixed-point z sums overflowed (pass a smaller zexp); " : "",
+            (err & 4) ? "a Gamma draw failed (non-finite shape/scale or the rejection cap)" : "");
+    return -1;
+  }
+  if (fl)
+    warn("\nWARNING: %llu observation-sweeps hit a sampler cap or numerical guard in the resident chain\n", fl);
   return 0;
 }
 

@@ -51,10 +51,12 @@ struct SweepArgs {
   uint32_t *mbest;             /* [count * (1 + mhit)] */
   uint32_t *mq0, *mq1;         /* [count * (1 + mhit)] */
   unsigned *mcnt;              /* [kMhrsCounters] */
-  /* UNIF (pht_unif.h): the per-sweep table (written by unif_table_kernel)
-   * and its last row index K */
+  /* UNIF (pht_unif.h): the per-sweep table (written by unif_table_kernel),
+   * its capacity (last row index) and the shard's largest y: the table
+   * kernel sizes K from mu (known only on the device in a resident chain) */
   double *utab;
   int uK;
+  double uymax;
   /* debug per-observation outputs (DEBUG kernels only) */
   long long *dbg_zq;           /* [count*n] */
   int *dbg_N;                  /* [count*n*n] */
@@ -62,8 +64,34 @@ struct SweepArgs {
   uint32_t *dbg_ndraw;
 };
 
+/* the device-resident chain's per-sweep update (pht_resident.hip); all
+ * pointers are device memory.  Parameter maps (GibbsState's lists,
+ * gibbs_host.cpp) as CSR: entries of parameter k at [off[k], off[k+1]) in
+ * insertion order (the update visits them in reverse, as the host does). */
+struct ResidentArgs {
+  int n, m, it, init;
+  double zs;                    /* 2^-zexp */
+  long long expect;             /* observations per sweep, node-wide (< 0: unchecked) */
+  uint32_t k0, k1;              /* Philox key of the Gamma streams (include/pht_gamma.h) */
+  const double *nu, *zeta;      /* [m] */
+  const double *start;          /* [m], or nullptr: prior mode / prior draw */
+  const int *nl_off, *nl_idx;   /* N counts of parameter k: stats[2n + idx] */
+  const int *zl_off, *zl_i;     /* z sums: z[i] / c */
+  const double *zl_c;
+  const int *tl_off, *tl_ij;    /* TT cells (i + j (n+1)) = theta_k c */
+  const double *tl_c;
+  const int *dl_off, *dl_ij;    /* per row i: its TT cells (the diagonal) */
+  unsigned long long *stats;    /* the sweep's block, read then zeroed */
+  double *TT;                   /* (n+1)^2, zero outside the parameter cells */
+  double *res;                  /* [it * m], res[iter + k it] */
+  unsigned char *params;        /* the packed block the next sweep reads */
+  unsigned long long *flagged;  /* flagged observation-sweeps, accumulated */
+  int *err;                     /* bit 0: count, bit 1: z overflow, bit 2: Gamma draw */
+};
+
 }  // namespace pht
 
+extern "C" hipError_t pht_launch_resident_update(const pht::ResidentArgs *r, int iter, hipStream_t st);
 extern "C" hipError_t pht_launch_sweep(const pht::SweepArgs *a, int method, int debug, hipStream_t st);
 extern "C" hipError_t pht_launch_ecs_chains(const pht::SweepArgs *h, const pht::SweepArgs *d, int K, hipStream_t st);
 

@@ -1087,9 +1087,8 @@ __global__ void __launch_bounds__(kUnifTabThreads) unif_table_kernel(SweepArgs a
   const int n = nval<NT>(a.n);
   const Layout L = make_layout(n);
   const double *d = reinterpret_cast<const double *>(a.params);
-  const int K = a.uK;
+  __shared__ int Ksh;
   double *T = a.utab;
-  double *invk = T + 4, *ax = invk + (K + 1), *ac = ax + (K + 1), *A = ac + (K + 1);
   const int tid = threadIdx.x, nt = blockDim.x;
   if (tid == 0) {
     double mu = 0.0;
@@ -1099,11 +1098,19 @@ __global__ void __launch_bounds__(kUnifTabThreads) unif_table_kernel(SweepArgs a
     }
     hdr[0] = mu;
     hdr[1] = 1.0 / mu;
+    /* rows: the shard's largest lam with a Poisson margin, within the
+     * capacity a.uK (the host's sizing; rows beyond it flag, never bias) */
+    const double lmax = mu * a.uymax;
+    const double kd = ceil(lmax + 14.0 * sqrt(lmax) + 64.0);
+    Ksh = (kd < (double)a.uK) ? (int)kd : a.uK;
     T[0] = mu;
     T[1] = hdr[1];
-    T[2] = (double)K;
+    T[2] = (double)Ksh;
     T[3] = 0.0;
   }
+  __syncthreads();
+  const int K = Ksh;
+  double *invk = T + 4, *ax = invk + (K + 1), *ac = ax + (K + 1), *A = ac + (K + 1);
   for (int k = tid; k <= K; k += nt) invk[k] = k ? 1.0 / (double)k : 0.0;
   if (tid < n) A[tid] = d[L.pi + tid];
   __syncthreads();
@@ -1167,8 +1174,8 @@ __global__ void __launch_bounds__(kBlock) unif_kernel(SweepArgs a) {
   PHT_LDS unsigned *Nc = Bc + n;
   PHT_LDS int *cursor = (PHT_LDS int *)(Nc + n * n);
   PHT_LDS double *tl = (PHT_LDS double *)(lsm + ((pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 15) & ~15));
-  const int K = a.uK;
   const double *T = a.utab;
+  const int K = (int)T[2]; /* rows of this sweep's table (<= a.uK, the LDS sizing) */
   for (int k = threadIdx.x; k < 3 * (K + 1); k += blockDim.x) tl[k] = T[4 + k];
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;

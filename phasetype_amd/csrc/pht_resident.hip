@@ -1,0 +1,162 @@
+/*
+ * pht_resident.hip — the device-resident Gibbs chain's per-sweep update
+ * (opt-in, NON-PARITY): everything LJMA_Gibbs does on the
+ * host between two step-1 sweeps, as one workgroup, so sweeps chain on the
+ * stream with no host round trip:
+ *
+ *   step 4-5 (src/PHT_MCMC_Aslett.c:340-397): Nsum/zsum per parameter from
+ *     the (reduced) statistics block in the reference's list order, the
+ *     conjugate draw Gamma(nu + Nsum, 1 / (zeta + zsum)) — counter-based
+ *     (include/pht_gamma.h) instead of R's rgamma — the TT/S/s refresh and
+ *     the diagonal in reverse list order;
+ *   step 1's setup (src/PHT_MCMC_Aslett.c:279-297): the packed parameter
+ *     block of the next sweep (P, Pfull, exit data, candidate lists) with
+ *     build_params's arithmetic; no eigensystem (the resident chain runs the
+ *     eigen-free samplers: UNIF and MHRS);
+ *   the checks of the host loop (processed count, z overflow), into an
+ *     error word; flagged observations accumulated.
+ * init = 1: iteration 0 (GibbsState's constructor: the start row, or the
+ * prior mode / prior draw, and the forward-order diagonal).
+ */
+#include <hip/hip_runtime.h>
+
+#include "pht_detmath.h"
+#include "pht_gamma.h"
+#include "pht_kernels.h"
+#include "pht_layout.h"
+
+namespace pht {
+
+constexpr int kResThreads = 256;
+constexpr int kResMaxM = (kMaxN + 1) * (kMaxN + 1);
+
+__global__ void __launch_bounds__(kResThreads) resident_update_kernel(ResidentArgs r, int iter) {
+  __shared__ double theta[kResMaxM];
+  pht_stage_math_tables();
+  const int n = r.n, n1 = n + 1, m = r.m, tid = threadIdx.x;
+  const int sl = stats_len(n);
+  const unsigned long long *st = r.stats;
+  __syncthreads();
+  if (!r.init) {
+    if (tid == 0) {
+      const unsigned long long *xw = st + 2 * n + n * n;
+      if (r.expect >= 0 && (long long)xw[kXObs] != r.expect) atomicOr(r.err, 1);
+      if (xw[kXOverflow] != 0ull) atomicOr(r.err, 2);
+      if (xw[kXFlagged] != 0ull) atomicAdd(r.flagged, xw[kXFlagged]);
+    }
+    for (int k = tid; k < m; k += blockDim.x) {
+      long long nsum = 0;
+      for (int e = r.nl_off[k + 1] - 1; e >= r.nl_off[k]; e--) nsum += (long long)st[2 * n + r.nl_idx[e]];
+      double zsum = 0.0;
+      for (int e = r.zl_off[k + 1] - 1; e >= r.zl_off[k]; e--) {
+        const long long q = (long long)st[r.zl_i[e]];
+        if (q < 0) atomicOr(r.err, 2);
+        zsum += ((double)q * r.zs) / r.zl_c[e];
+      }
+      pht_stream s;
+      pht_stream_init(&s, r.k0, r.k1, PHT_GAMMA_OBS(k), PHT_GAMMA_TAG, (uint32_t)iter);
+      const double th = pht_rgamma_ctr(&s, r.nu[k] + (double)(int)nsum, 1.0 / (r.zeta[k] + zsum));
+      if (!(th > 0.0) || !isfinite(th)) atomicOr(r.err, 4);
+      r.res[iter + (long)k * r.it] = th;
+      theta[k] = th;
+    }
+  } else {
+    for (int k = tid; k < m; k += blockDim.x) {
+      double th;
+      if (r.start) {
+        th = r.start[k];
+      } else if (r.nu[k] > 1) {
+        th = (r.nu[k] - 1.0) / r.zeta[k];
+      } else {
+        pht_stream s;
+        pht_stream_init(&s, r.k0, r.k1, PHT_GAMMA_OBS(k), PHT_GAMMA_TAG, 0u);
+        th = pht_rgamma_ctr(&s, r.nu[k], 1.0 / r.zeta[k]);
+      }
+      r.res[(long)k * r.it] = th;
+      theta[k] = th;
+    }
+  }
+  __syncthreads();
+  /* TT cells of every parameter (each cell belongs to one parameter) */
+  for (int k = tid; k < m; k += blockDim.x)
+    for (int e = r.tl_off[k]; e < r.tl_off[k + 1]; e++) r.TT[r.tl_ij[e]] = theta[k] * r.tl_c[e];
+  __syncthreads();
+  /* the diagonal: the constructor sums a row forward, the update in reverse
+   * list order (GibbsState, gibbs_host.cpp) */
+  if (tid < n) {
+    const int i = tid;
+    double d = 0.0;
+    if (r.init) {
+      for (int e = r.dl_off[i]; e < r.dl_off[i + 1]; e++) d -= r.TT[r.dl_ij[e]];
+    } else {
+      for (int e = r.dl_off[i + 1] - 1; e >= r.dl_off[i]; e--) d -= r.TT[r.dl_ij[e]];
+    }
+    r.TT[i + i * n1] = d;
+  }
+  __syncthreads();
+  /* the next sweep's parameter block (build_params without the eigensystem) */
+  const Layout L = make_layout(n);
+  double *dv = reinterpret_cast<double *>(r.params);
+  int *iv = reinterpret_cast<int *>(r.params + L.ndouble * 8);
+  if (tid < n) {
+    const int i = tid;
+    const double *TT = r.TT;
+    double *P = dv + L.P, *Pf = dv + L.Pf;
+    for (int j = 0; j < n; j++) dv[L.S + i + j * n] = TT[i + j * n1];
+    const double si = TT[i + n * n1];
+    dv[L.s + i] = si;
+    dv[L.pi + i] = (i == 0) ? 1.0 : 0.0;
+    const double Sii = TT[i + i * n1];
+    double rsum, rsumfull = 0.0;
+    for (int j = 0; j < n; j++) {
+      const double v = -TT[i + j * n1] / Sii;
+      P[i + j * n] = v;
+      Pf[i + j * n] = v;
+      rsumfull += v;
+    }
+    rsum = rsumfull - P[i + i * n];
+    {
+      const double v = -si / Sii;
+      Pf[i + n * n] = v;
+      rsumfull += v;
+    }
+    rsumfull -= Pf[i + i * n];
+    Pf[i + i * n] = 0.0;
+    P[i + i * n] = 0.0;
+    for (int j = 0; j < n; j++) {
+      P[i + j * n] = P[i + j * n] / rsum;
+      Pf[i + j * n] = Pf[i + j * n] / rsumfull;
+    }
+    Pf[i + n * n] = Pf[i + n * n] / rsumfull;
+    dv[L.logs + i] = si > 0.0 ? pht_log(si) : 0.0;
+    const double sc = 1.0 / -Sii;
+    dv[L.scale + i] = sc;
+    dv[L.logscale + i] = pht_log(sc);
+  }
+  __syncthreads();
+  if (tid < n) {
+    const int j = tid;
+    const double *P = dv + L.P, *Pf = dv + L.Pf, *S = dv + L.S;
+    int a = 0, b = 0, c = 0;
+    for (int k = 0; k < n; k++) {
+      if (!(P[j + k * n] == 0.0)) iv[L.succP + j * n + a++] = k;
+      if (k != j && !(S[j + k * n] == 0.0)) iv[L.succS + j * n + c++] = k;
+    }
+    for (int k = 0; k <= n; k++)
+      if (!(Pf[j + k * n] == 0.0)) iv[L.succPf + j * (n + 1) + b++] = k;
+    iv[L.nsuccP + j] = a;
+    iv[L.nsuccPf + j] = b;
+    iv[L.nsuccS + j] = c;
+  }
+  /* the next sweep accumulates into a zeroed block */
+  for (int k = tid; k < sl; k += blockDim.x) r.stats[k] = 0ull;
+}
+
+}  // namespace pht
+
+extern "C" hipError_t pht_launch_resident_update(const pht::ResidentArgs *r, int iter, hipStream_t st) {
+  using namespace pht;
+  if (r->n < 1 || r->n > kMaxN || r->m < 1 || r->m > kResMaxM) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(resident_update_kernel, dim3(1), dim3(kResThreads), 0, st, *r, iter);
+  return hipGetLastError();
+}

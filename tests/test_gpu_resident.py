@@ -1,0 +1,103 @@
+"""GPU: the device-resident Gibbs chain (pht_gibbs_run_resident; SURVEY.md
+§8f.1-2, opt-in, non-parity): sweeps, conjugate Gamma updates and parameter
+blocks all on the device, one host wait per run.
+
+* bit for bit against the oracle's restatement of the same chain (oracle
+  gibbs dev=2: the GPU spec's sweeps + include/pht_gamma.h draws), UNIF and
+  MHRS, with censoring;
+* in distribution against the reference: posterior means and quantiles
+  within 5 combined MCSEs of tests/golden/g5_posterior.npz (UNIF against the
+  reference's ECS chains — the same conditional path law — and MHRS against
+  the reference's MHRS chains);
+* the guards: eigen-based samplers refused, the processed-count check.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import phasetype_amd as P
+from oracle import posterior as PO
+from phasetype_amd.synth import bd_exit, bd_exit_structure, simulate_ph
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "g5_posterior.npz")
+
+
+@pytest.mark.parametrize("method,n,mhit,cf", [(8, 6, 1, 0.3), (8, 10, 1, 0.0), (1, 4, 1, 0.3), (1, 4, 3, 0.0),
+                                              (8, 15, 1, 0.3)])
+def test_resident_chain_bitexact(gpu, orc, method, n, mhit, cf):
+    T, theta = bd_exit_structure(n)
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 3000, seed=21 + n, censor_frac=cf)
+    m, it = len(theta), 25
+    nu, zeta = 1 + 50 * theta, np.full(m, 50.0)
+    Cm = np.ones_like(T, dtype=np.float64)
+    orc.set_seed(123)
+    want = orc.gibbs(2, it, mhit, method, n, nu, zeta, T.reshape(-1, order="F"), Cm.reshape(-1, order="F"), y, cen)
+    P.set_seed(123)
+    sw = P.Sweeper(n, method, mhit)
+    sw.set_obs(y, cen)
+    got = sw.gibbs_resident(it, method, nu, zeta, T, Cm, P.zexp_for(y))
+    assert np.array_equal(got, want), np.abs(got - want).max()
+    P.set_seed(123)
+    again = sw.gibbs_resident(it, method, nu, zeta, T, Cm, P.zexp_for(y))
+    assert np.array_equal(got, again)
+    sw.close()
+
+
+def test_resident_start_and_small_prior_shapes(gpu, orc):
+    """A user start row; and priors with nu <= 1 (drawn, not the mode)."""
+    n, method = 5, 8
+    T, theta = bd_exit_structure(n)
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 2000, seed=3)
+    m, it = len(theta), 8
+    Cm = np.ones_like(T, dtype=np.float64)
+    for nu, zeta, start in ((1 + 50 * theta, np.full(m, 50.0), theta * 1.2),
+                            (np.full(m, 0.8), np.full(m, 0.5), None)):
+        orc.set_seed(9)
+        want = orc.gibbs(2, it, 1, method, n, nu, zeta, T.reshape(-1, order="F"), Cm.reshape(-1, order="F"), y, cen,
+                         start=start)
+        P.set_seed(9)
+        sw = P.Sweeper(n, method, 1)
+        sw.set_obs(y, cen)
+        got = sw.gibbs_resident(it, method, nu, zeta, T, Cm, P.zexp_for(y), start=start)
+        sw.close()
+        assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("name,method", [("n10_ecs", 8), ("n15_cens_ecs", 8), ("n20_ecs", 8), ("cfg1_mhrs", 1),
+                                         ("n15_cens_mhrs", 1)])
+def test_resident_chain_matches_reference_posterior(gpu, name, method):
+    n, _, mhit, y, cen, T, nu, zeta = PO.case_inputs(name)
+    ref = PO.unpack(np.load(GOLD), name)
+    sw = P.Sweeper(n, method, mhit)
+    sw.set_obs(y, cen)
+    P.set_seed(1618)
+    chain = sw.gibbs_resident(9001, method, nu, zeta, T, np.ones(T.shape), P.zexp_for(y))
+    sw.close()
+    ok, worst, bad = PO.compare(PO.summarize(chain), ref)
+    assert ok, (name, worst, bad[:5])
+    assert sw.flagged_obs == 0
+
+
+def test_resident_guards(gpu):
+    n = 4
+    T, theta = bd_exit_structure(n)
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 1000, seed=4)
+    m = len(theta)
+    nu, zeta, Cm = 1 + 50 * theta, np.full(m, 50.0), np.ones(T.shape)
+    sw = P.Sweeper(n, 2, 1)
+    sw.set_obs(y, cen)
+    with pytest.raises(P.PhaseTypeError, match="eigen-free"):
+        sw.gibbs_resident(5, 2, nu, zeta, T, Cm, P.zexp_for(y))
+    sw.close()
+    sw = P.Sweeper(n, 8, 1)
+    sw.set_obs(y, cen)
+    sw.set_global_count(len(y) + 5)
+    with pytest.raises(P.PhaseTypeError, match="did not sample every observation"):
+        sw.gibbs_resident(5, 8, nu, zeta, T, Cm, P.zexp_for(y))
+    sw.close()
