@@ -118,6 +118,8 @@ class OracleLib:
         L.orc_zexp.argtypes = [_dp, C.c_long]
         L.orc_gibbs.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _dp,
                                 _dp, C.c_long, _ip, _dp, _dp]
+        L.orc_gibbs_z.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _dp,
+                                  _dp, C.c_long, _ip, _dp, _dp, C.c_int]
         L.orc_rgamma_ctr_v.argtypes = [C.c_uint32, C.c_uint32, C.c_double, C.c_double, C.c_long, _dp]
 
     def set_seed(self, seed: int) -> None:
@@ -174,6 +176,15 @@ class OracleLib:
             out.update(B=B, pre=pre, z=z.reshape(l, n), zq=zqo.reshape(l, n),
                        N=N.reshape(l, n, n).transpose(0, 2, 1), flags=fl, ndraw=nd)
         return out
+
+    def gibbs_zexp(self, dev, it, mhit, method, n, nu, zeta, T, C_, y, censored, zexp, start=None):
+        """gibbs() at an explicit fixed-point exponent (dev variants)."""
+        if start is None:
+            start = np.array([-1.0])
+        a = gibbs_argv(it, mhit, method, n, nu, zeta, T, C_, y, censored, start, 1)
+        self.lib.orc_gibbs_z(int(dev), it, mhit, method, n, len(nu), a["nu"], a["zeta"], a["T"], a["C"], a["y"],
+                             len(y), a["censored"], a["start"], a["res"], int(zexp))
+        return a["res"].reshape(len(nu), it).T.copy()
 
     def rgamma_ctr(self, a, scale, cnt, key=(1, 2)):
         """cnt draws of the device-resident chain's Gamma sampler (include/pht_gamma.h)."""

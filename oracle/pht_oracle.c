@@ -471,16 +471,19 @@ typedef struct { int i, j; double c; } ent;
  * as arrays visited in the lists' (reverse-insertion) order, which fixes the
  * floating summation order of zsum and of the diagonal refresh.
  */
-void orc_gibbs(int dev, int it, int mhit, int method, int n, int m, const double *nu, const double *zeta,
-               const int *T, const double *C, const double *y, long l, const int *censored, const double *start,
-               double *res) {
+/* zexp_in: the fixed-point exponent (dev variants), or ORC_ZEXP_AUTO for
+ * orc_zexp(y) as the product's LJMA_Gibbs takes it */
+#define ORC_ZEXP_AUTO (-100000)
+void orc_gibbs_z(int dev, int it, int mhit, int method, int n, int m, const double *nu, const double *zeta,
+                 const int *T, const double *C, const double *y, long l, const int *censored, const double *start,
+                 double *res, int zexp_in) {
   const int n1 = n + 1;
   uint32_t k0 = 0, k1 = 0;
   int zexp = 0;
   if (dev) {
     k0 = (uint32_t)(pht_rs_unif_rand(&g_rs) * 4294967296.0);
     k1 = (uint32_t)(pht_rs_unif_rand(&g_rs) * 4294967296.0);
-    zexp = orc_zexp(y, l);
+    zexp = zexp_in == ORC_ZEXP_AUTO ? orc_zexp(y, l) : zexp_in;
   }
   double *TT = (double *)calloc((size_t)n1 * n1, sizeof(double));
   double S[ORC_MAXN * ORC_MAXN], s[ORC_MAXN];
@@ -588,6 +591,12 @@ void orc_gibbs(int dev, int it, int mhit, int method, int n, int m, const double
   for (int i = 0; i < n1; i++) free(Dl[i]);
   free(Nl); free(Sl); free(sl); free(zl); free(TTl); free(Dl);
   free(nN); free(nS); free(ns); free(nz); free(nTT); free(nD);
+}
+
+void orc_gibbs(int dev, int it, int mhit, int method, int n, int m, const double *nu, const double *zeta,
+               const int *T, const double *C, const double *y, long l, const int *censored, const double *start,
+               double *res) {
+  orc_gibbs_z(dev, it, mhit, method, n, m, nu, zeta, T, C, y, l, censored, start, res, ORC_ZEXP_AUTO);
 }
 
 /* primitive probes for tests/test_detmath.py and tests/test_philox.py */

@@ -409,7 +409,7 @@ constexpr long kSpreadLanes = 256L * 2 * 256;
  * for it.
  */
 struct ChainGroup {
-  int K = 0, device = 0, n = 0, pb = 0, sl = 0;
+  int K = 0, device = 0, n = 0, pb = 0, sl = 0, method = kMethodECS;
   std::mutex m;
   std::condition_variable cv;
   int active = 0;
@@ -446,9 +446,10 @@ static void group_destroy(ChainGroup *g) {
   delete g;
 }
 
-static ChainGroup *group_create(int device, int K, int n) {
+static ChainGroup *group_create(int device, int K, int n, int method) {
   ChainGroup *g = new ChainGroup();
   g->K = K;
+  g->method = method;
   g->device = device;
   g->n = n;
   g->pb = make_layout(n).bytes();
@@ -456,7 +457,7 @@ static ChainGroup *group_create(int device, int K, int n) {
   g->active = K;
   g->ex.resize(K);
   g->ce.resize(K);
-  const size_t P = (size_t)g->pb * K, Sb = sizeof(unsigned long long) * g->sl * K, A = sizeof(SweepArgs) * K;
+  const size_t P = (size_t)g->pb * K, Sb = sizeof(unsigned long long) * g->sl * K, A = sizeof(SweepArgs) * 2 * K;
   const bool ok = hipSetDevice(device) == hipSuccess &&
                   hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) == hipSuccess &&
                   hipEventCreate(&g->ev0) == hipSuccess && hipEventCreate(&g->ev1) == hipSuccess &&
@@ -484,23 +485,33 @@ static void group_fire(ChainGroup *g) {
     e = hipMemsetAsync(g->d_stats, 0, sizeof(unsigned long long) * g->sl * g->K, g->stream);
   if (e == hipSuccess) e = hipEventRecord(g->ev0, g->stream);
   int nx = 0, nc = 0;
-  for (int i = 0; i < k; i++) {
-    const int w = g->who[i];
-    if (g->ex[w].count > 0) g->h_args[nx++] = g->ex[w];
-    if (g->ce[w].count > 0) nc++;
+  if (g->method == kMethodECS) {
+    /* exact ranges [0, K), censored ranges [K, 2K) of the packed arguments */
+    for (int i = 0; i < k; i++) {
+      const int w = g->who[i];
+      if (g->ex[w].count > 0) g->h_args[nx++] = g->ex[w];
+    }
+    for (int i = 0; i < k; i++) {
+      const int w = g->who[i];
+      if (g->ce[w].count > 0) g->h_args[g->K + nc++] = g->ce[w];
+    }
+  } else {
+    for (int i = 0; i < k; i++)
+      if (g->ex[g->who[i]].count > 0) g->h_args[nx++] = g->ex[g->who[i]];
   }
-  /* censored ranges on stream2 while the exact ranges run (as ctx_enqueue) */
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(g->d_args, g->h_args, sizeof(SweepArgs) * 2 * g->K, hipMemcpyHostToDevice, g->stream);
+  /* ECS: every chain's censored range in one launch on stream2 while the
+   * exact ranges run (as ctx_enqueue) */
   const bool fork = nc > 0 && nx > 0;
   if (e == hipSuccess && fork) e = hipEventRecord(g->evf, g->stream);
   if (e == hipSuccess && fork) e = hipStreamWaitEvent(g->stream2, g->evf, 0);
-  for (int i = 0; i < k && e == hipSuccess; i++) {
-    const int w = g->who[i];
-    if (g->ce[w].count > 0) e = pht_launch_sweep(&g->ce[w], kMethodECS, 0, fork ? g->stream2 : g->stream);
-  }
+  if (e == hipSuccess && nc > 0)
+    e = pht_launch_chains(g->h_args + g->K, g->d_args + g->K, nc, kMethodECS, fork ? g->stream2 : g->stream);
   if (e == hipSuccess && fork) e = hipEventRecord(g->evj, g->stream2);
   if (e == hipSuccess && nx > 0)
-    e = hipMemcpyAsync(g->d_args, g->h_args, sizeof(SweepArgs) * nx, hipMemcpyHostToDevice, g->stream);
-  if (e == hipSuccess && nx > 0) e = pht_launch_ecs_chains(g->h_args, g->d_args, nx, g->stream);
+    e = g->method == kMethodECS ? pht_launch_ecs_chains(g->h_args, g->d_args, nx, g->stream)
+                                : pht_launch_chains(g->h_args, g->d_args, nx, g->method, g->stream);
   if (e == hipSuccess && fork) e = hipStreamWaitEvent(g->stream, g->evj, 0);
   if (e == hipSuccess) e = hipEventRecord(g->ev1, g->stream);
   if (e == hipSuccess)
@@ -512,6 +523,8 @@ static void group_fire(ChainGroup *g) {
   g->gen++;
   g->cv.notify_all();
 }
+
+static int unif_prepare(pht_ctx *c, SweepArgs &a);
 
 /* chain c's sweep (parameters in c->h_params): returns when the group's sweep
  * is done, with c->h_stats and c->last_ms filled */
@@ -532,16 +545,28 @@ static int group_sweep(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   a.sweep = sweep;
   a.zscale = ldexp(1.0, zexp);
   a.stats = ds;
-  SweepArgs ae = a;
-  ae.begin = 0;
-  ae.count = c->n_exact;
-  ae.newcap = getenv("PHT_NEWCAP") ? atoi(getenv("PHT_NEWCAP")) : 1;
-  ae.spread = getenv("PHT_SPREAD") ? atoi(getenv("PHT_SPREAD")) : (c->n_exact <= 2 * kSpreadLanes);
-  SweepArgs ac = a;
-  ac.cens = c->d_cens;
-  ac.begin = c->n_exact;
-  ac.count = c->count - c->n_exact;
-  ac.allcens = 1;
+  SweepArgs ae = a, ac = a;
+  if (g->method == kMethodECS) {
+    ae.begin = 0;
+    ae.count = c->n_exact;
+    ae.newcap = getenv("PHT_NEWCAP") ? atoi(getenv("PHT_NEWCAP")) : 1;
+    ae.spread = getenv("PHT_SPREAD") ? atoi(getenv("PHT_SPREAD")) : (c->n_exact <= 2 * kSpreadLanes);
+    ac.cens = c->d_cens;
+    ac.begin = c->n_exact;
+    ac.count = c->count - c->n_exact;
+    ac.allcens = 1;
+  } else {
+    /* the whole shard in one argument (MHRS, DCS, UNIF) */
+    ae.begin = 0;
+    ae.count = c->count;
+    ae.cens = c->d_cens;
+    ae.mbest = c->d_mbest;
+    ae.mq0 = c->d_mq0;
+    ae.mq1 = c->d_mq1;
+    ae.mcnt = c->d_mcnt;
+    if (g->method == kMethodUNIF && unif_prepare(c, ae)) return -1;
+    ac.count = 0;
+  }
   std::unique_lock<std::mutex> lk(g->m);
   memcpy(g->h_params + (size_t)g->pb * w, c->h_params, g->pb);
   g->ex[w] = ae;
@@ -867,6 +892,34 @@ static long exact_rowk(const pht_ctx *c) {
   return 0;                                  /* cfg4's 10^6: rows cost the one-lane range more (K = 64: +1 %) */
 }
 
+/* UNIF: size (and grow) the context's table for this sweep's parameters
+ * (c->h_params): the shard's largest lam = mu y with a Poisson margin
+ * (pht_unif.h); observations beyond it are flagged, never wrong */
+static int unif_prepare(pht_ctx *c, SweepArgs &a) {
+  const Layout L = make_layout(c->n);
+  const double *S = reinterpret_cast<const double *>(c->h_params) + L.S;
+  double mu = 0.0;
+  for (int i = 0; i < c->n; i++) mu = std::max(mu, -S[i + i * c->n]);
+  if (!(mu > 0.0) || !std::isfinite(mu)) {
+    set_err("UNIF: the generator's largest exit rate is %g (need a positive finite rate)", mu);
+    return -1;
+  }
+  const double lmax = mu * c->ymax;
+  const double kd = std::ceil(lmax + 14.0 * std::sqrt(lmax) + 64.0);
+  a.uK = (int)std::min<double>(kUnifMaxK, std::isfinite(kd) ? kd : (double)kUnifMaxK);
+  a.uymax = c->ymax;
+  const long need = unif_tab_doubles(c->n, a.uK);
+  if (need > c->utab_cap) {
+    if (c->d_utab) HIPCHK(hipFree(c->d_utab));
+    c->d_utab = nullptr;
+    const long cap = std::max(need, unif_tab_doubles(c->n, std::min(kUnifMaxK, a.uK * 3 / 2)));
+    HIPCHK(hipMalloc(&c->d_utab, sizeof(double) * cap));
+    c->utab_cap = cap;
+  }
+  a.utab = c->d_utab;
+  return 0;
+}
+
 static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int zexp, bool debug) {
   HIPCHK(hipSetDevice(c->device));
   const int pb = make_layout(c->n).bytes();
@@ -918,31 +971,7 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     a.dbg_flags = c->d_flags;
     a.dbg_ndraw = c->d_ndraw;
   }
-  if (c->method == kMethodUNIF) {
-    /* table length: the shard's largest lam = mu y with a Poisson margin
-     * (pht_unif.h); observations beyond it are flagged, never wrong */
-    const Layout L = make_layout(c->n);
-    const double *S = reinterpret_cast<const double *>(c->h_params) + L.S;
-    double mu = 0.0;
-    for (int i = 0; i < c->n; i++) mu = std::max(mu, -S[i + i * c->n]);
-    if (!(mu > 0.0) || !std::isfinite(mu)) {
-      set_err("UNIF: the generator's largest exit rate is %g (need a positive finite rate)", mu);
-      return -1;
-    }
-    const double lmax = mu * c->ymax;
-    const double kd = std::ceil(lmax + 14.0 * std::sqrt(lmax) + 64.0);
-    a.uK = (int)std::min<double>(kUnifMaxK, std::isfinite(kd) ? kd : (double)kUnifMaxK);
-    a.uymax = c->ymax;
-    const long need = unif_tab_doubles(c->n, a.uK);
-    if (need > c->utab_cap) {
-      if (c->d_utab) HIPCHK(hipFree(c->d_utab));
-      c->d_utab = nullptr;
-      const long cap = std::max(need, unif_tab_doubles(c->n, std::min(kUnifMaxK, a.uK * 3 / 2)));
-      HIPCHK(hipMalloc(&c->d_utab, sizeof(double) * cap));
-      c->utab_cap = cap;
-    }
-    a.utab = c->d_utab;
-  }
+  if (c->method == kMethodUNIF && unif_prepare(c, a)) return -1;
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   if (c->method == kMethodECS) {
     /* exact observations: persistent ECS kernel; censored: LJMA_samplechain path */
@@ -1347,18 +1376,20 @@ extern "C" int pht_gibbs_run_chains(pht_ctx **ctxs, int nchains, const uint32_t 
       set_err("pht_gibbs_run_chains: context %d is null or has an RCCL communicator attached", c);
       return -1;
     }
-  /* exact ECS ranges of all chains in one launch per sweep, when the chains
-   * share a device and n (PHT_CHAINS_LAUNCH=streams: one launch per chain) */
+  /* all chains' sweeps in one launch sequence, when the chains share a
+   * device, n and method (ECS: the exact ranges in one ecs_chains_kernel and
+   * the censored ranges in one cens_chains_kernel; MHRS/DCS/UNIF: one
+   * launch_chains sequence); PHT_CHAINS_LAUNCH=streams: a launch per chain */
   ChainGroup *grp = nullptr;
   {
     bool one = nchains >= 2;
     for (int c = 0; c < nchains && one; c++)
-      one = ctxs[c]->method == kMethodECS && ctxs[c]->device == ctxs[0]->device && ctxs[c]->n == ctxs[0]->n &&
+      one = ctxs[c]->method == ctxs[0]->method && ctxs[c]->device == ctxs[0]->device && ctxs[c]->n == ctxs[0]->n &&
             !ctxs[c]->grp;
     const char *ev = getenv("PHT_CHAINS_LAUNCH");
     if (ev && !strcmp(ev, "streams")) one = false;
     if (one) {
-      grp = group_create(ctxs[0]->device, nchains, ctxs[0]->n);
+      grp = group_create(ctxs[0]->device, nchains, ctxs[0]->n, ctxs[0]->method);
       if (!grp) {
         set_err("pht_gibbs_run_chains: HIP allocation failed");
         return -1;

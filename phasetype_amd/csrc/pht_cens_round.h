@@ -24,7 +24,7 @@
 namespace pht {
 
 template <int NT, bool DEBUG>
-__device__ __forceinline__ void cens_round_body(const SweepArgs &a) {
+__device__ __forceinline__ void cens_round_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
   const Layout L = make_layout(n);
@@ -62,7 +62,7 @@ __device__ __forceinline__ void cens_round_body(const SweepArgs &a) {
     /* ---- a free lane takes the next observation and starts its path */
     if (!have && !done) {
       const long tk = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const long p = claim_pos(tk);
+      const long p = claim_pos(tk, blk, nblk);
       if (p >= a.count) {
         done = true;
       } else {

@@ -121,7 +121,7 @@ struct DcsLane {
  * (claim_pos).  LDS: parameter block, accumulators, cursor, near masks.
  */
 template <int NT, bool DEBUG>
-__device__ __forceinline__ void dcs_round_body(const SweepArgs &a) {
+__device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
   const Layout L = make_layout(n);
@@ -179,7 +179,6 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a) {
   unsigned c_witer = 0, c_wround = 0;
   auto __lane_id_first = [&]() { return __lane_id() == (unsigned)__builtin_ctzll(__ballot(1)); };
 #endif
-  const unsigned blk = blockIdx.x, nblk = gridDim.x;
 
   /* observation complete: counters, debug rows; the lane is free again */
   auto finish_obs = [&]() {

@@ -12,7 +12,9 @@
 #define PHT_DECL(K) \
   extern "C" hipError_t pht_launch_nt_##K(const pht::SweepArgs *a, int method, int debug, hipStream_t st); \
   extern "C" hipError_t pht_launch_chains_nt_##K(const pht::SweepArgs *h, const pht::SweepArgs *d, int nch, \
-                                                 hipStream_t st);
+                                                 hipStream_t st);                                            \
+  extern "C" hipError_t pht_launch_mchains_nt_##K(const pht::SweepArgs *h, const pht::SweepArgs *d, int nch,  \
+                                                  int method, hipStream_t st);
 PHT_DECL(0)
 PHT_DECL(3)
 PHT_DECL(5)
@@ -54,5 +56,27 @@ extern "C" hipError_t pht_launch_ecs_chains(const pht::SweepArgs *h, const pht::
     case 15: return pht_launch_chains_nt_15(h, d, K, st);
     case 20: return pht_launch_chains_nt_20(h, d, K, st);
     default: return pht_launch_chains_nt_0(h, d, K, st);
+  }
+}
+
+/* K chains' sweeps in one launch sequence for MHRS, DCS, UNIF (whole
+ * shards) or ECS's censored ranges; see launch_chains */
+extern "C" hipError_t pht_launch_chains(const pht::SweepArgs *h, const pht::SweepArgs *d, int K, int method,
+                                        hipStream_t st) {
+  using namespace pht;
+  if (K < 1) return hipErrorInvalidValue;
+  const int n = h[0].n;
+  if (n < 1 || n > kMaxN || (make_layout(n).bytes() & 15) != 0) return hipErrorInvalidValue;
+  for (int c = 0; c < K; c++)
+    if (h[c].n != n || h[c].dbg_zq != nullptr) return hipErrorInvalidValue;
+  static const bool generic = getenv("PHT_FORCE_NT0") != nullptr;
+  if (generic) return pht_launch_mchains_nt_0(h, d, K, method, st);
+  switch (n) {
+    case 3: return pht_launch_mchains_nt_3(h, d, K, method, st);
+    case 5: return pht_launch_mchains_nt_5(h, d, K, method, st);
+    case 10: return pht_launch_mchains_nt_10(h, d, K, method, st);
+    case 15: return pht_launch_mchains_nt_15(h, d, K, method, st);
+    case 20: return pht_launch_mchains_nt_20(h, d, K, method, st);
+    default: return pht_launch_mchains_nt_0(h, d, K, method, st);
   }
 }

@@ -159,14 +159,14 @@ __device__ __forceinline__ Par<NT> stage_params(const SweepArgs &a, PHT_LDS unsi
  * mhrs_compact.
  */
 template <int NT, int W, int K>
-__global__ void __launch_bounds__(kBlock) mhrs_search(SweepArgs a, uint32_t A0, const uint32_t *qin,
-                                                      const unsigned *cin) {
+__device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0, const uint32_t *qin,
+                                                 const unsigned *cin, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int T1 = 1 + a.mhit;
   const long total = (qin ? (long)(*cin) : a.count * T1) * W;
   /* block b owns claim chunks b, b + grid, ...: none when b * 64 >= total
    * (small shards, empty rounds): leave before staging anything */
-  if ((long)blockIdx.x * kClaimChunk >= total) return;
+  if ((long)blk * kClaimChunk >= total) return;
   const Par<NT> P = stage_params<NT>(a, (PHT_LDS unsigned char *)smem);
   /* items are claimed one at a time through an LDS cursor (claim_pos: the
    * block's 64-item chunks), so a lane whose item ends takes the next one
@@ -192,7 +192,7 @@ __global__ void __launch_bounds__(kBlock) mhrs_search(SweepArgs a, uint32_t A0, 
     while (!inatt) { /* next attempt of this item, or the next item */
       if (!have) {
         if (item >= total) break;
-        item = claim_pos(__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        item = claim_pos(__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), blk, nblk);
         if (item >= total) break;
         const long q = item / W;
         l = (int)(item % W);
@@ -277,16 +277,26 @@ __global__ void __launch_bounds__(kBlock) mhrs_search(SweepArgs a, uint32_t A0, 
   }
 }
 
-/* tasks of qin still unresolved -> qout (templated only to keep one copy
- * per pht_kernels_nt.hip unit) */
-template <int NT>
-__global__ void __launch_bounds__(kBlock) mhrs_compact(SweepArgs a, const uint32_t *qin, const unsigned *cin,
-                                                       uint32_t *qout, unsigned *cout) {
+template <int NT, int W, int K>
+__global__ void __launch_bounds__(kBlock) mhrs_search(SweepArgs a, uint32_t A0, const uint32_t *qin,
+                                                      const unsigned *cin) {
+  mhrs_search_body<NT, W, K>(a, A0, qin, cin, blockIdx.x, gridDim.x);
+}
+
+/* tasks of qin still unresolved -> qout */
+__device__ __forceinline__ void mhrs_compact_body(const SweepArgs &a, const uint32_t *qin, const unsigned *cin,
+                                                  uint32_t *qout, unsigned *cout, unsigned blk, unsigned nblk) {
   const long cnt = qin ? (long)(*cin) : a.count * (1 + a.mhit);
-  for (long q = (long)blockIdx.x * kBlock + threadIdx.x; q < cnt; q += (long)gridDim.x * kBlock) {
+  for (long q = (long)blk * kBlock + threadIdx.x; q < cnt; q += (long)nblk * kBlock) {
     const uint32_t task = qin ? qin[q] : (uint32_t)q;
     if (a.mbest[task] == kMhrsUnresolved) qout[atomicAdd(cout, 1u)] = task;
   }
+}
+/* (templated only to keep one copy per pht_kernels_nt.hip unit) */
+template <int NT>
+__global__ void __launch_bounds__(kBlock) mhrs_compact(SweepArgs a, const uint32_t *qin, const unsigned *cin,
+                                                       uint32_t *qout, unsigned *cout) {
+  mhrs_compact_body(a, qin, cin, qout, cout, blockIdx.x, gridDim.x);
 }
 
 /* LJMA_MHsample_Bladt's MH step over the chains' first successes, then the
@@ -338,7 +348,7 @@ __device__ __forceinline__ void mhrs_finish(const Par<NT> &P, const SweepArgs &a
  * slot through an LDS cursor as soon as its observation is done, so a
  * wavefront never waits on its longest path; DCS and the censored range). */
 template <int NT, int METHOD, bool DEBUG, class Env, bool PERSIST = false>
-__device__ __forceinline__ void sweep_body(const SweepArgs &a) {
+__device__ __forceinline__ void sweep_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
   const Layout L = make_layout(n);
@@ -366,11 +376,11 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
   P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
   P.Lr = L;
 
-  long i = a.begin + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long i = a.begin + (long)blk * blockDim.x + threadIdx.x;
   for (;;) {
     if (PERSIST) {
       const long t = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const long p = claim_pos(t);
+      const long p = claim_pos(t, blk, nblk);
       if (p >= a.count) break;
       i = a.begin + p;
     } else if (i >= a.begin + a.count) {
@@ -417,7 +427,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a) {
 
 template <int NT, int METHOD, bool DEBUG>
 __global__ void __launch_bounds__(kBlock) sweep_kernel(SweepArgs a) {
-  sweep_body<NT, METHOD, DEBUG, EnvPrivate>(a);
+  sweep_body<NT, METHOD, DEBUG, EnvPrivate>(a, blockIdx.x, gridDim.x);
 }
 
 /* waves per SIMD the persistent kernel is compiled for: the DCS kernel at
@@ -440,7 +450,7 @@ template <int NT, int METHOD, bool DEBUG>
 __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(persist_waves<NT, METHOD>())))
 persist_kernel(SweepArgs a) {
-  sweep_body<NT, METHOD, DEBUG, EnvPrivate, true>(a);
+  sweep_body<NT, METHOD, DEBUG, EnvPrivate, true>(a, blockIdx.x, gridDim.x);
 }
 #endif
 
@@ -1037,7 +1047,7 @@ template <int NT, bool DEBUG>
 __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(dcs_waves<NT>())))
 dcs_round_kernel(SweepArgs a) {
-  dcs_round_body<NT, DEBUG>(a);
+  dcs_round_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
 }
 template <int NT, bool DEBUG>
 static hipError_t launch_dcs_round(const SweepArgs &a, hipStream_t st) {
@@ -1059,7 +1069,7 @@ template <int NT, bool DEBUG>
 __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(persist_waves<NT, kMethodECS>())))
 cens_round_kernel(SweepArgs a) {
-  cens_round_body<NT, DEBUG>(a);
+  cens_round_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
 }
 template <int NT, bool DEBUG>
 static hipError_t launch_cens_round(const SweepArgs &a, hipStream_t st) {
@@ -1081,7 +1091,7 @@ static hipError_t launch_cens_round(const SweepArgs &a, hipStream_t st) {
  * (rows [2^i, 2^(i+1)) from rows [0, 2^i) and P_i), then ax, ac, invk. */
 constexpr int kUnifTabThreads = 1024;
 template <int NT>
-__global__ void __launch_bounds__(kUnifTabThreads) unif_table_kernel(SweepArgs a) {
+__device__ __forceinline__ void unif_table_body(const SweepArgs &a) {
   __shared__ double Pm[2][kMaxN * kMaxN];
   __shared__ double hdr[2];
   const int n = nval<NT>(a.n);
@@ -1154,18 +1164,23 @@ __global__ void __launch_bounds__(kUnifTabThreads) unif_table_kernel(SweepArgs a
   }
 }
 
+template <int NT>
+__global__ void __launch_bounds__(kUnifTabThreads) unif_table_kernel(SweepArgs a) {
+  unif_table_body<NT>(a);
+}
+
 /* UNIF sweep: persistent lanes, one observation per lane to its end
  * (claims as the other persistent kernels: 64-position chunks through an
  * LDS cursor), exact and censored observations in one launch */
 static int smem_bytes_unif(int n, int K) { return ((smem_bytes(n) + 15) & ~15) + 3 * (K + 1) * 8; }
 
 template <int NT, bool DEBUG>
-__global__ void __launch_bounds__(kBlock) unif_kernel(SweepArgs a) {
+__device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
   const Layout L = make_layout(n);
   const int pbytes = L.bytes();
-  if ((long)blockIdx.x * kClaimChunk >= a.count) return;
+  if ((long)blk * kClaimChunk >= a.count) return;
   const Par<NT> P = stage_params<NT>(a, (PHT_LDS unsigned char *)smem);
   PHT_LDS unsigned char *lsm = (PHT_LDS unsigned char *)smem;
   PHT_LDS unsigned long long *zq = (PHT_LDS unsigned long long *)(lsm + pbytes);
@@ -1193,7 +1208,7 @@ __global__ void __launch_bounds__(kBlock) unif_kernel(SweepArgs a) {
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
   unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
   for (;;) {
-    const long p = claim_pos(__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    const long p = claim_pos(__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), blk, nblk);
     if (p >= a.count) break;
     const long i = a.begin + p;
     Lane ln;
@@ -1227,6 +1242,11 @@ __global__ void __launch_bounds__(kBlock) unif_kernel(SweepArgs a) {
 }
 
 template <int NT, bool DEBUG>
+__global__ void __launch_bounds__(kBlock) unif_kernel(SweepArgs a) {
+  unif_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
+}
+
+template <int NT, bool DEBUG>
 static hipError_t launch_unif(const SweepArgs &a, hipStream_t st) {
   if (a.utab == nullptr || a.uK < 1 || a.uK > kUnifMaxK || a.begin != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL((unif_table_kernel<NT>), dim3(1), dim3(kUnifTabThreads), 0, st, a);
@@ -1256,6 +1276,154 @@ static bool cens_legacy() {
 static bool dcs_legacy() {
   static const bool v = env_legacy("PHT_DCS_KERNEL");
   return v;
+}
+
+/* ====================================== several chains in one launch (§8f.4)
+ * Block b of a chains launch serves chain b % K as its block b / K of nblk
+ * (the bodies take their block index and count), staging that chain's
+ * parameters and adding into that chain's statistics.  An observation's
+ * result depends only on (its id, the chain's key, sweep and parameters), so
+ * every chain equals its own single launch bit for bit. */
+template <int NT>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(dcs_waves<NT>())))
+dcs_chains_kernel(const SweepArgs *args, int K, unsigned nblk) {
+  dcs_round_body<NT, false>(args[blockIdx.x % (unsigned)K], blockIdx.x / (unsigned)K, nblk);
+}
+template <int NT>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(persist_waves<NT, kMethodECS>())))
+cens_chains_kernel(const SweepArgs *args, int K, unsigned nblk) {
+  cens_round_body<NT, false>(args[blockIdx.x % (unsigned)K], blockIdx.x / (unsigned)K, nblk);
+}
+template <int NT>
+__global__ void __launch_bounds__(kUnifTabThreads) unif_table_chains_kernel(const SweepArgs *args) {
+  unif_table_body<NT>(args[blockIdx.x]);
+}
+template <int NT>
+__global__ void __launch_bounds__(kBlock) unif_chains_kernel(const SweepArgs *args, int K, unsigned nblk) {
+  unif_body<NT, false>(args[blockIdx.x % (unsigned)K], blockIdx.x / (unsigned)K, nblk);
+}
+/* MHRS: per chain, the first-success records to "unresolved" and the queue
+ * counters to zero (grid-stride over each chain's tasks) */
+template <int NT> /* (templated only to keep one copy per pht_kernels_nt.hip unit) */
+__global__ void __launch_bounds__(kBlock) mhrs_init_chains(const SweepArgs *args, int K, unsigned nblk) {
+  const SweepArgs &a = args[blockIdx.x % (unsigned)K];
+  const unsigned blk = blockIdx.x / (unsigned)K;
+  const long tasks = a.count * (1 + a.mhit);
+  for (long q = (long)blk * kBlock + threadIdx.x; q < tasks; q += (long)nblk * kBlock) a.mbest[q] = kMhrsUnresolved;
+  if (blk == 0 && threadIdx.x < kMhrsCounters) a.mcnt[threadIdx.x] = 0u;
+}
+/* search round r (0..5) of every chain: round r >= 1 reads the queue the
+ * compaction after round r - 1 wrote (launch_mhrs_search's sequence) */
+template <int NT, int W, int KA>
+__global__ void __launch_bounds__(kBlock) mhrs_search_chains(const SweepArgs *args, int K, unsigned nblk, int r,
+                                                             uint32_t A0) {
+  const SweepArgs &a = args[blockIdx.x % (unsigned)K];
+  const uint32_t *qin = r == 0 ? nullptr : ((r & 1) ? a.mq0 : a.mq1);
+  const unsigned *cin = r == 0 ? nullptr : a.mcnt + (r - 1);
+  mhrs_search_body<NT, W, KA>(a, A0, qin, cin, blockIdx.x / (unsigned)K, nblk);
+}
+template <int NT>
+__global__ void __launch_bounds__(kBlock) mhrs_compact_chains(const SweepArgs *args, int K, unsigned nblk, int r) {
+  const SweepArgs &a = args[blockIdx.x % (unsigned)K];
+  const uint32_t *qin = r == 0 ? nullptr : ((r & 1) ? a.mq0 : a.mq1);
+  const unsigned *cin = r == 0 ? nullptr : a.mcnt + (r - 1);
+  mhrs_compact_body(a, qin, cin, (r & 1) ? a.mq1 : a.mq0, a.mcnt + r, blockIdx.x / (unsigned)K, nblk);
+}
+template <int NT>
+__global__ void __launch_bounds__(kBlock) mhrs_finish_chains(const SweepArgs *args, int K, unsigned nblk) {
+  const SweepArgs &a = args[blockIdx.x % (unsigned)K];
+  const unsigned blk = blockIdx.x / (unsigned)K;
+  if ((long)blk * kBlock >= a.count) return; /* the whole block: its chain has fewer observations */
+  sweep_body<NT, kMethodMHRS, false, EnvPrivate>(a, blk, nblk);
+}
+
+/* h: the chains' arguments on the host (sizing), d: the same K SweepArgs on
+ * the device.  ECS: the censored ranges (allcens); the exact ranges use
+ * launch_ecs_chains.  MHRS, DCS, UNIF: whole shards (begin = 0). */
+template <int NT>
+static hipError_t launch_chains(const SweepArgs *h, const SweepArgs *d, int K, int method, hipStream_t st) {
+  long maxc = 0;
+  for (int c = 0; c < K; c++) maxc = std::max(maxc, h[c].count);
+  auto share = [&](int occ, int cus, long want) -> long { /* blocks per chain */
+    long nb = std::max(1L, (long)cus * occ / K);
+    return std::min(nb, std::max(1L, want));
+  };
+  if (method == kMethodECS) {
+    static LaunchCfg cfg;
+    const int sm = smem_bytes(h[0].n);
+    int occ = 0, cus = 0;
+    if (hipError_t e = launch_config(cfg, (const void *)cens_chains_kernel<NT>, sm, &occ, &cus); e != hipSuccess)
+      return e;
+    const long nb = share(occ, cus, (maxc + kClaimChunk - 1) / kClaimChunk);
+    hipLaunchKernelGGL((cens_chains_kernel<NT>), dim3((unsigned)(nb * K)), dim3(kBlock), sm, st, d, K, (unsigned)nb);
+    return hipGetLastError();
+  }
+  if (method == kMethodDCS) {
+    static LaunchCfg cfg;
+    const int sm = dcs_smem_bytes(make_layout(h[0].n).bytes(), h[0].n);
+    int occ = 0, cus = 0;
+    if (hipError_t e = launch_config(cfg, (const void *)dcs_chains_kernel<NT>, sm, &occ, &cus); e != hipSuccess)
+      return e;
+    const long nb = share(occ, cus, (maxc + kClaimChunk - 1) / kClaimChunk);
+    hipLaunchKernelGGL((dcs_chains_kernel<NT>), dim3((unsigned)(nb * K)), dim3(kBlock), sm, st, d, K, (unsigned)nb);
+    return hipGetLastError();
+  }
+  if (method == kMethodUNIF) {
+    int uK = 0;
+    for (int c = 0; c < K; c++) {
+      if (h[c].utab == nullptr || h[c].uK < 1 || h[c].uK > kUnifMaxK) return hipErrorInvalidValue;
+      uK = std::max(uK, h[c].uK);
+    }
+    hipLaunchKernelGGL((unif_table_chains_kernel<NT>), dim3((unsigned)K), dim3(kUnifTabThreads), 0, st, d);
+    if (maxc < 1) return hipGetLastError();
+    static LaunchCfg cfg;
+    const int sm = smem_bytes_unif(h[0].n, uK);
+    int occ = 0, cus = 0;
+    if (hipError_t e = launch_config(cfg, (const void *)unif_chains_kernel<NT>, sm, &occ, &cus); e != hipSuccess)
+      return e;
+    const long nb = share(occ, cus, (maxc + kClaimChunk - 1) / kClaimChunk);
+    hipLaunchKernelGGL((unif_chains_kernel<NT>), dim3((unsigned)(nb * K)), dim3(kBlock), sm, st, d, K, (unsigned)nb);
+    return hipGetLastError();
+  }
+  if (method == kMethodMHRS) {
+    long maxt = 0;
+    for (int c = 0; c < K; c++) {
+      if (h[c].mbest == nullptr || h[c].mq0 == nullptr || h[c].mq1 == nullptr || h[c].mcnt == nullptr || h[c].begin)
+        return hipErrorInvalidValue;
+      maxt = std::max(maxt, h[c].count * (1 + h[c].mhit));
+    }
+    if (maxc < 1) return hipSuccess;
+    const int smc = make_layout(h[0].n).bytes() + 16;
+    static LaunchCfg cfg;
+    int occ = 0, cus = 0;
+    if (hipError_t e = launch_config(cfg, (const void *)mhrs_search_chains<NT, 1, kMhrsK0>, smc, &occ, &cus);
+        e != hipSuccess)
+      return e;
+    const long nbi = std::max(1L, std::min(1024L / K + 1, (maxt + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL((mhrs_init_chains<NT>), dim3((unsigned)(nbi * K)), dim3(kBlock), 0, st, d, K, (unsigned)nbi);
+    const long nb = std::max(1L, (long)cus * occ / K); /* persistent: the resident blocks, shared */
+    const dim3 g((unsigned)(nb * K));
+    const long nbc = std::max(1L, 256L / K);
+    const dim3 gc((unsigned)(nbc * K));
+    constexpr MhrsRound R1 = kMhrsRounds[0], R2 = kMhrsRounds[1], R3 = kMhrsRounds[2], R4 = kMhrsRounds[3],
+                        R5 = kMhrsRounds[4];
+    hipLaunchKernelGGL((mhrs_search_chains<NT, 1, kMhrsK0>), g, dim3(kBlock), smc, st, d, K, (unsigned)nb, 0, 0u);
+    hipLaunchKernelGGL((mhrs_compact_chains<NT>), gc, dim3(kBlock), 0, st, d, K, (unsigned)nbc, 0);
+    hipLaunchKernelGGL((mhrs_search_chains<NT, R1.W, R1.K>), g, dim3(kBlock), smc, st, d, K, (unsigned)nb, 1, R1.A0);
+    hipLaunchKernelGGL((mhrs_compact_chains<NT>), gc, dim3(kBlock), 0, st, d, K, (unsigned)nbc, 1);
+    hipLaunchKernelGGL((mhrs_search_chains<NT, R2.W, R2.K>), g, dim3(kBlock), smc, st, d, K, (unsigned)nb, 2, R2.A0);
+    hipLaunchKernelGGL((mhrs_compact_chains<NT>), gc, dim3(kBlock), 0, st, d, K, (unsigned)nbc, 2);
+    hipLaunchKernelGGL((mhrs_search_chains<NT, R3.W, R3.K>), g, dim3(kBlock), smc, st, d, K, (unsigned)nb, 3, R3.A0);
+    hipLaunchKernelGGL((mhrs_compact_chains<NT>), gc, dim3(kBlock), 0, st, d, K, (unsigned)nbc, 3);
+    hipLaunchKernelGGL((mhrs_search_chains<NT, R4.W, R4.K>), g, dim3(kBlock), smc, st, d, K, (unsigned)nb, 4, R4.A0);
+    hipLaunchKernelGGL((mhrs_compact_chains<NT>), gc, dim3(kBlock), 0, st, d, K, (unsigned)nbc, 4);
+    hipLaunchKernelGGL((mhrs_search_chains<NT, R5.W, R5.K>), g, dim3(kBlock), smc, st, d, K, (unsigned)nb, 5, R5.A0);
+    const long nbf = (maxc + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL((mhrs_finish_chains<NT>), dim3((unsigned)(nbf * K)), dim3(kBlock), smem_bytes(h[0].n), st, d,
+                       K, (unsigned)nbf);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
 }
 
 template <int NT>

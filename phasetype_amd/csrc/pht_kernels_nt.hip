@@ -21,3 +21,8 @@ extern "C" hipError_t PHT_CAT(pht_launch_chains_nt_, PHT_NT)(const pht::SweepArg
                                                             hipStream_t st) {
   return pht::launch_ecs_chains<PHT_NT>(h, d, K, st);
 }
+
+extern "C" hipError_t PHT_CAT(pht_launch_mchains_nt_, PHT_NT)(const pht::SweepArgs *h, const pht::SweepArgs *d, int K,
+                                                             int method, hipStream_t st) {
+  return pht::launch_chains<PHT_NT>(h, d, K, method, st);
+}

@@ -20,7 +20,7 @@ from phasetype_amd.synth import DATA_KEY, bd_exit, bd_exit_structure, simulate_p
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--Ks", nargs="+", type=int, default=[1, 2, 4, 8])
-    ap.add_argument("--cfgs", nargs="+", default=["cfg1:3:200:ECS", "cfg2:5:10000:ECS", "cfg2m:5:10000:MHRS"])
+    ap.add_argument("--cfgs", nargs="+", default=["cfg1:3:200:ECS", "cfg2:5:10000:ECS", "cfg2m:5:10000:MHRS", "cfg2d:5:10000:DCS", "cfg2u:5:10000:UNIF"])
     a = ap.parse_args()
     for spec in a.cfgs:
         name, n, N, meth = spec.split(":")
