@@ -177,23 +177,31 @@ __device__ __forceinline__ void round_invert(Env &e, const double *cs, double pr
   const double xl = e.X(q - 1), xr = e.X(q);
   const double yr = e.Y(q), yl = e.Y(q - 1);
   const double eyr = expshift(yr, e.ymax);
+  /* the point is built in scalars and stored once: assigning p's fields in
+   * both branches let the compiler merge them into one store through a
+   * selected field address, which put p (and its reloads) in scratch every
+   * round (r03: ~167 scratch stores per wave per sweep at cfg4) */
+  double px, py, pey;
   if (xl == xr) {
-    p.x = xr; p.y = yr; p.ey = eyr;
-    return;
-  }
-  const double eyl = expshift(yl, e.ymax);
-  if (fabs(yr - yl) < kYEps) {
-    if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
-      p.x = xl + (PHT_DIV((xr - xl), (eyr - eyl))) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
-    else
-      p.x = xl + (xr - xl) * prop;
-    p.ey = (PHT_DIV((p.x - xl), (xr - xl))) * (eyr - eyl) + eyl;
-    p.y = logshift(p.ey, e.ymax);
+    px = xr; py = yr; pey = eyr;
   } else {
-    p.x = xl + (PHT_DIV((xr - xl), (yr - yl))) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
-    p.y = (PHT_DIV((p.x - xl), (xr - xl))) * (yr - yl) + yl;
-    p.ey = expshift(p.y, e.ymax);
+    const double eyl = expshift(yl, e.ymax);
+    if (fabs(yr - yl) < kYEps) {
+      if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
+        px = xl + (PHT_DIV((xr - xl), (eyr - eyl))) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
+      else
+        px = xl + (xr - xl) * prop;
+      pey = (PHT_DIV((px - xl), (xr - xl))) * (eyr - eyl) + eyl;
+      py = logshift(pey, e.ymax);
+    } else {
+      px = xl + (PHT_DIV((xr - xl), (yr - yl))) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
+      py = (PHT_DIV((px - xl), (xr - xl))) * (yr - yl) + yl;
+      pey = expshift(py, e.ymax);
+    }
   }
+  p.x = px;
+  p.y = py;
+  p.ey = pey;
 }
 
 /* the first half of arms_update (shift + insert + XEPS adjustment), for an

@@ -638,6 +638,9 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
   };
   /* per-lane observation counters, flushed once at the end */
   unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
+#ifdef PHT_ECS_DIAG
+  unsigned c_big = 0, c_wbig = 0, c_wround = 0, c_act = 0;
+#endif
   for (;;) {
     bool need = false;
     topup(!pend);
@@ -710,6 +713,20 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
 #ifdef PHT_STAMPS
     ln.st_rounds++;
 #endif
+#ifdef PHT_ECS_DIAG
+    /* diagnostic builds: lane-rounds in the general ARMS code (envelope
+     * beyond kRoundCap), wave-rounds with at least one such lane, wave-rounds,
+     * lane-rounds with a sojourn to sample (extra words 6, 7, 8, 9) */
+    {
+      const bool bigl = pend && env.cnt + 2 > kRoundCap;
+      c_big += bigl ? 1u : 0u;
+      c_act += (need || pend) ? 1u : 0u;
+      if ((threadIdx.x & 63) == 0) {
+        c_wbig += __any(bigl) ? 1u : 0u;
+        c_wround++;
+      }
+    }
+#endif
     topup(need || pend);
     PHT_STAMP(ln, 12);
     ecs_round(P, ln, env, sk, st, need, pend, pd, lam);
@@ -727,6 +744,12 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
   lds_add(&xc[2], (unsigned long long)c_flag);
   lds_add(&xc[3], (unsigned long long)c_nd);
   lds_add(&xc[4], (unsigned long long)c_jump);
+#endif
+#ifdef PHT_ECS_DIAG
+  lds_add(&xc[6], (unsigned long long)c_big);
+  lds_add(&xc[7], (unsigned long long)c_wbig);
+  lds_add(&xc[8], (unsigned long long)c_wround);
+  lds_add(&xc[9], (unsigned long long)c_act);
 #endif
   __syncthreads();
   flush_stats(a.stats, zq, Bc, Nc, xc, n);

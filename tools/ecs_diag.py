@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""ECS round diagnostics from a -D PHT_ECS_DIAG variant build (PHT_LIB):
+how often lanes run the general ARMS code (envelope beyond the converged
+round's 13 points) and how many wave-rounds that divergence touches.
+usage (GPU box): PHT_LIB=phasetype_amd/_variants/diag.so python3 tools/ecs_diag.py [--n 10 --N 1000000]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import phasetype_amd as P  # noqa: E402
+from phasetype_amd.synth import DATA_KEY, bd_exit, simulate_ph  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=10)
+ap.add_argument("--N", type=int, default=1_000_000)
+a = ap.parse_args()
+S, s = bd_exit(a.n)
+y, cen = simulate_ph(S, s, a.N, seed=DATA_KEY)
+sw = P.Sweeper(a.n, 2)
+sw.set_obs(y, cen)
+st = sw.sweep(S, s, key=(1, 2), sweep=1, zexp=P.zexp_for(y))
+_, _, _, ex = P.split_stats(st, a.n)
+print(json.dumps({"n": a.n, "N": a.N, "kernel_ms": sw.last_kernel_ms(), "obs": int(ex[0]), "jumps": int(ex[4]),
+                  "lane_rounds_big": int(ex[6]), "wave_rounds_with_big": int(ex[7]), "wave_rounds": int(ex[8]),
+                  "lane_rounds_active": int(ex[9]),
+                  "frac_wave_rounds_with_big": float(ex[7]) / max(1.0, float(ex[8])),
+                  "big_per_jump": float(ex[6]) / max(1.0, float(ex[4]))}))

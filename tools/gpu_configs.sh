@@ -16,3 +16,13 @@ run cfg4_mhrs --n 10 --N 1000000 --method MHRS --steps 10
 run cfg5_mhrs --n 15 --N 500000 --censor 0.3 --method MHRS --steps 10
 run cfg5_dcs --n 15 --N 500000 --censor 0.3 --method DCS --steps 5
 run cfg5_ecs --n 15 --N 500000 --censor 0.3 --method ECS --steps 10
+run cfg3_unif --n 20 --N 100000 --method UNIF --steps 50
+run cfg5_unif --n 15 --N 500000 --censor 0.3 --method UNIF --steps 20
+python3 - $O <<'PY'
+import json, sys, glob, os
+for f in sorted(glob.glob(os.path.join(sys.argv[1], "cfg*.json"))):
+    d = json.load(open(f))
+    alt = d.get("alt_sampler") or {}
+    print(f"{os.path.basename(f)[:-5]:12s} {d['value']:9.1f} sweeps/s  ms/step {d['ms_per_step']:.4f}  kernel {d['roofline']['kernel_ms']:.4f}"
+          + (f"  | UNIF {alt['value']:.1f}" if alt else ""))
+PY

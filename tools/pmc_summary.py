@@ -11,7 +11,7 @@ import sys
 from collections import defaultdict
 
 
-def main(d, out=None, kernel_sub="pht::"):
+def main(d, out=None, kernel_sub=os.environ.get("PMC_KERNEL", "ecs_exact_kernel")):
     acc = defaultdict(list)
     bench = None
     for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
@@ -68,7 +68,7 @@ def write_traffic(res, bench, path, src):
          "hbm_read_bytes_corrected": der.get("hbm_read_bytes_corrected"),
          "hbm_write_bytes": der.get("hbm_write_bytes"),
          "fp64_flops_per_launch": der.get("fp64_flops_per_launch"),
-         "kernel": "pht::ecs_exact_kernel (sum over the sweep's pht:: dispatches)",
+         "kernel": "pht::ecs_exact_kernel",
          "source": src,
          "method_note": "FETCH_SIZE x 2 (gfx950 wide-read correction) x 1024 + WRITE_SIZE x 1024, "
                         "per-dispatch averages from separate --pmc passes (MI355X_MICROARCH.md HBM)"}

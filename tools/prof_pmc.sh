@@ -12,7 +12,7 @@ while read -r GROUP; do
   [ -z "$GROUP" ] && continue
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $GROUP --output-format csv -d $OUT/p$i -o run -- \
-    python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline "$@" > $OUT/p$i.bench.json 2> $OUT/p$i.err || exit $?
+    python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-alt "$@" > $OUT/p$i.bench.json 2> $OUT/p$i.err || exit $?
   echo "pass $i done: $GROUP"
 done <<'GROUPS'
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU
