@@ -307,24 +307,31 @@ static void orc_unif_obs(const orc_sp *sp, const double *T, double y, int cens, 
       if (c2 >= t2) { js = j; break; }
     }
     b = js;
-    double tm = y, tend = y;
+    double lt = 0.0, tend = y;
     for (int m = ks; m >= 1; m--) { /* the bridge, backward */
-      tm = tm * pht_exp_neg(pht_log(pht_next_u(r)) * invk[m]);
+      lt = fma(pht_log(pht_next_u(r)), invk[m], lt);
       const double *Am = A + (long)(m - 1) * n;
-      double tot = 0.0;
-      for (int c = 0; c < n; c++) tot = fma(Am[c], orc_unif_R(sp, rinv, c, b), tot);
+      const double tot = A[(long)m * n + b]; /* = sum_c A_{m-1}[c] R_cb */
       const double tg = pht_next_u(r) * tot;
-      int cs = b;
-      if (tot > 0.0) {
+      int cs = -1;
+      if (tot > 0.0) { /* predecessors of b: R_cb > 0, increasing c */
+        int last = -1;
         double cum2 = 0.0;
         for (int c = 0; c < n; c++) {
-          cum2 = fma(Am[c], orc_unif_R(sp, rinv, c, b), cum2);
+          const double v = orc_unif_R(sp, rinv, c, b);
+          if (!(v > 0.0)) continue;
+          cum2 = fma(Am[c], v, cum2);
+          if (Am[c] > 0.0) last = c;
           if (cum2 >= tg) { cs = c; break; }
         }
-      } else {
+        if (cs < 0) cs = last;
+      }
+      if (cs < 0) {
         o->flags |= ORC_FLAG_UNIF;
+        cs = b;
       }
       if (cs != b) {
+        const double tm = y * pht_exp_neg(lt);
         orcD_zadd(o, b, tend - tm, zscale);
         o->N[cs + b * n]++;
         tend = tm;

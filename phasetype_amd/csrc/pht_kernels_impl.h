@@ -22,6 +22,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <mutex>
 
 #include "pht_device.h"
@@ -1113,10 +1114,40 @@ static hipError_t launch_cens_round(const SweepArgs &a, hipStream_t st) {
  * mu, R and its squarings in LDS, the forward vectors A_k by doubling
  * (rows [2^i, 2^(i+1)) from rows [0, 2^i) and P_i), then ax, ac, invk. */
 constexpr int kUnifTabThreads = 1024;
-template <int NT>
+/* the forward vectors in LDS while they are built (one dependent LDS
+ * round trip per doubling step instead of an L2 one), when (K+1) n doubles
+ * fit this budget; else in the global table directly */
+constexpr int kUnifTabLds = 128 * 1024;
+template <class APtr>
+__device__ __forceinline__ void unif_doubling(APtr A, double (*Pm)[kMaxN * kMaxN], int n, int K) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  int cur = 0;
+  for (int p = 1; p <= K; p <<= 1) {
+    /* rows p + r, r < p, from rows r and P = Pm[cur] (= R^p) */
+    const int rows = (K - p + 1 < p) ? K - p + 1 : p;
+    for (int e = tid; e < rows * n; e += nt) {
+      const int r = e / n, j = e % n;
+      double acc = 0.0;
+      for (int c = 0; c < n; c++) acc = fma(A[(long)r * n + c], Pm[cur][c + j * n], acc);
+      A[(long)(p + r) * n + j] = acc;
+    }
+    if (2 * p <= K) { /* P_{i+1} = P_i P_i */
+      for (int e = tid; e < n * n; e += nt) {
+        const int c = e % n, j = e / n;
+        double acc = 0.0;
+        for (int q = 0; q < n; q++) acc = fma(Pm[cur][c + q * n], Pm[cur][q + j * n], acc);
+        Pm[cur ^ 1][e] = acc;
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+template <int NT, bool LDSA>
 __device__ __forceinline__ void unif_table_body(const SweepArgs &a) {
   __shared__ double Pm[2][kMaxN * kMaxN];
   __shared__ double hdr[2];
+  extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
   const Layout L = make_layout(n);
   const double *d = reinterpret_cast<const double *>(a.params);
@@ -1144,60 +1175,63 @@ __device__ __forceinline__ void unif_table_body(const SweepArgs &a) {
   __syncthreads();
   const int K = Ksh;
   double *invk = T + 4, *ax = invk + (K + 1), *ac = ax + (K + 1), *A = ac + (K + 1);
+  PHT_LDS double *Al = (PHT_LDS double *)smem;
   for (int k = tid; k <= K; k += nt) invk[k] = k ? 1.0 / (double)k : 0.0;
-  if (tid < n) A[tid] = d[L.pi + tid];
-  __syncthreads();
+  if (tid < n) {
+    if (LDSA) Al[tid] = d[L.pi + tid];
+    else A[tid] = d[L.pi + tid];
+  }
   const double rinv = hdr[1];
   for (int e = tid; e < n * n; e += nt) { /* Pm[0][c + j n] = R_cj */
     const int c = e % n, j = e / n;
     Pm[0][e] = (c == j) ? fma(d[L.S + c + c * n], rinv, 1.0) : d[L.S + c + j * n] * rinv;
   }
   __syncthreads();
-  int cur = 0;
-  for (int p = 1; p <= K; p <<= 1) {
-    /* rows p + r, r < p, from rows r and P = Pm[cur] (= R^p) */
-    const int rows = (K - p + 1 < p) ? K - p + 1 : p;
-    for (int e = tid; e < rows * n; e += nt) {
-      const int r = e / n, j = e % n;
-      const double *Ar = A + (long)r * n;
-      double acc = 0.0;
-      for (int c = 0; c < n; c++) acc = fma(Ar[c], Pm[cur][c + j * n], acc);
-      A[(long)(p + r) * n + j] = acc;
-    }
-    if (2 * p <= K) { /* P_{i+1} = P_i P_i */
-      for (int e = tid; e < n * n; e += nt) {
-        const int c = e % n, j = e / n;
-        double acc = 0.0;
-        for (int q = 0; q < n; q++) acc = fma(Pm[cur][c + q * n], Pm[cur][q + j * n], acc);
-        Pm[cur ^ 1][e] = acc;
-      }
-    }
-    __syncthreads();
-    cur ^= 1;
-  }
+  if (LDSA) unif_doubling(Al, Pm, n, K);
+  else unif_doubling(A, Pm, n, K);
+  if (LDSA)
+    for (long e = tid; e < (long)(K + 1) * n; e += nt) A[e] = Al[e];
   for (int k = tid; k <= K; k += nt) {
-    const double *Ak = A + (long)k * n;
     double sx = 0.0, sc = 0.0;
     for (int j = 0; j < n; j++) {
-      sx = fma(Ak[j], d[L.s + j], sx);
-      sc = sc + Ak[j];
+      const double v = LDSA ? Al[(long)k * n + j] : A[(long)k * n + j];
+      sx = fma(v, d[L.s + j], sx);
+      sc = sc + v;
     }
     ax[k] = sx;
     ac[k] = sc;
   }
 }
 
-template <int NT>
+template <int NT, bool LDSA>
 __global__ void __launch_bounds__(kUnifTabThreads) unif_table_kernel(SweepArgs a) {
-  unif_table_body<NT>(a);
+  unif_table_body<NT, LDSA>(a);
+}
+/* the table launch: LDS working rows when they fit (capacity a.uK) */
+template <int NT>
+static hipError_t launch_unif_table(const SweepArgs &a, hipStream_t st) {
+  const long bytes = (long)(a.uK + 1) * a.n * 8;
+  if (bytes <= kUnifTabLds) {
+    static LaunchCfg cfg;
+    int occ = 0, cus = 0;
+    if (hipError_t e = launch_config(cfg, (const void *)unif_table_kernel<NT, true>, (int)bytes, &occ, &cus);
+        e != hipSuccess)
+      return e;
+    hipLaunchKernelGGL((unif_table_kernel<NT, true>), dim3(1), dim3(kUnifTabThreads), (int)bytes, st, a);
+  } else {
+    hipLaunchKernelGGL((unif_table_kernel<NT, false>), dim3(1), dim3(kUnifTabThreads), 0, st, a);
+  }
+  return hipGetLastError();
 }
 
 /* UNIF sweep: persistent lanes, one observation per lane to its end
  * (claims as the other persistent kernels: 64-position chunks through an
  * LDS cursor), exact and censored observations in one launch */
-static int smem_bytes_unif(int n, int K) { return ((smem_bytes(n) + 15) & ~15) + 3 * (K + 1) * 8; }
+static int smem_bytes_unif(int n, int K) {
+  return ((smem_bytes(n) + 15) & ~15) + 3 * (K + 1) * 8 + n * n * 12 + n * 4; /* + predecessor lists */
+}
 
-template <int NT, bool DEBUG>
+template <int NT, bool DEBUG, bool ALDS>
 __device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
@@ -1214,17 +1248,28 @@ __device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsi
   PHT_LDS double *tl = (PHT_LDS double *)(lsm + ((pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 15) & ~15));
   const double *T = a.utab;
   const int K = (int)T[2]; /* rows of this sweep's table (<= a.uK, the LDS sizing) */
-  for (int k = threadIdx.x; k < 3 * (K + 1); k += blockDim.x) tl[k] = T[4 + k];
+  /* invk, ax, ac (and with ALDS the forward vectors A) staged into LDS */
+  const long nstage = 3L * (K + 1) + (ALDS ? (long)(K + 1) * n : 0L);
+  for (long k = threadIdx.x; k < nstage; k += blockDim.x) tl[k] = T[4 + k];
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
   if (threadIdx.x == 0) *cursor = 0;
   pht_stage_math_tables();
   __syncthreads();
-  UnifTab U;
+  PHT_LDS double *pv = tl + nstage;
+  PHT_LDS int *pc = (PHT_LDS int *)(pv + n * n), *np = pc + n * n;
+  unif_preds<NT>(P, T[1], pv, pc, np);
+  __syncthreads();
+  typedef typename std::conditional<ALDS, const PHT_LDS double *, const double *>::type APtr;
+  UnifTab<APtr> U;
   U.invk = tl;
   U.ax = tl + (K + 1);
   U.ac = tl + 2 * (K + 1);
-  U.A = T + 4 + 3 * (K + 1);
+  if constexpr (ALDS) U.A = tl + 3 * (K + 1);
+  else U.A = T + 4 + 3 * (K + 1);
+  U.pv = pv;
+  U.pc = pc;
+  U.np = np;
   U.K = K;
   U.mu = T[0];
   U.rinv = T[1];
@@ -1264,25 +1309,37 @@ __device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsi
   flush_stats(a.stats, zq, Bc, Nc, xc, n);
 }
 
-template <int NT, bool DEBUG>
+template <int NT, bool DEBUG, bool ALDS>
 __global__ void __launch_bounds__(kBlock) unif_kernel(SweepArgs a) {
-  unif_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
+  unif_body<NT, DEBUG, ALDS>(a, blockIdx.x, gridDim.x);
 }
 
 template <int NT, bool DEBUG>
 static hipError_t launch_unif(const SweepArgs &a, hipStream_t st) {
   if (a.utab == nullptr || a.uK < 1 || a.uK > kUnifMaxK || a.begin != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((unif_table_kernel<NT>), dim3(1), dim3(kUnifTabThreads), 0, st, a);
+  if (hipError_t e = launch_unif_table<NT>(a, st); e != hipSuccess) return e;
   if (a.count < 1) return hipGetLastError();
-  static LaunchCfg cfg;
+  /* PHT_UNIF_ALDS=1: the forward vectors in LDS too (same results; measured
+   * no faster than L2-resident vectors at n = 10..20, r03 — so opt-in) */
+  static LaunchCfg cfg, cfgl;
   const int sm = smem_bytes_unif(a.n, a.uK);
-  int occ = 0, cus = 0;
-  if (hipError_t e = launch_config(cfg, (const void *)unif_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
+  const int sml = sm + (a.uK + 1) * a.n * 8;
+  int occ = 0, cus = 0, occl = 0, cusl = 0;
+  if (hipError_t e = launch_config(cfg, (const void *)unif_kernel<NT, DEBUG, false>, sm, &occ, &cus); e != hipSuccess)
     return e;
-  long grid = (long)cus * occ;
+  static const int force = getenv("PHT_UNIF_ALDS") ? atoi(getenv("PHT_UNIF_ALDS")) : -1;
+  bool alds = false;
+  if (force == 1 && sml <= 160 * 1024) {
+    if (hipError_t e = launch_config(cfgl, (const void *)unif_kernel<NT, DEBUG, true>, sml, &occl, &cusl);
+        e != hipSuccess)
+      return e;
+    alds = true;
+  }
+  long grid = (long)cus * (alds ? occl : occ);
   const long want = (a.count + kClaimChunk - 1) / kClaimChunk;
   if (grid > want) grid = want;
-  hipLaunchKernelGGL((unif_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
+  if (alds) hipLaunchKernelGGL((unif_kernel<NT, DEBUG, true>), dim3((unsigned)grid), dim3(kBlock), sml, st, a);
+  else hipLaunchKernelGGL((unif_kernel<NT, DEBUG, false>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
   return hipGetLastError();
 }
 
@@ -1319,11 +1376,11 @@ cens_chains_kernel(const SweepArgs *args, int K, unsigned nblk) {
 }
 template <int NT>
 __global__ void __launch_bounds__(kUnifTabThreads) unif_table_chains_kernel(const SweepArgs *args) {
-  unif_table_body<NT>(args[blockIdx.x]);
+  unif_table_body<NT, false>(args[blockIdx.x]);
 }
 template <int NT>
 __global__ void __launch_bounds__(kBlock) unif_chains_kernel(const SweepArgs *args, int K, unsigned nblk) {
-  unif_body<NT, false>(args[blockIdx.x % (unsigned)K], blockIdx.x / (unsigned)K, nblk);
+  unif_body<NT, false, false>(args[blockIdx.x % (unsigned)K], blockIdx.x / (unsigned)K, nblk);
 }
 /* MHRS: per chain, the first-success records to "unresolved" and the queue
  * counters to zero (grid-stride over each chain's tasks) */

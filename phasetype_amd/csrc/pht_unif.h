@@ -31,11 +31,17 @@
  *  2. The path on [0, y] given X_{k*} = j* is bridged BACKWARD with the
  *     forward vectors: X_{m-1} ~ A_{m-1}[c] R_{c,X_m} (m = k*, ..., 1), so
  *     no power table is needed; X_0 ~ pi comes out last (the start state B).
+ *     The normaliser is the table's A_m[X_m] (= sum_c A_{m-1}[c] R_{c,X_m});
+ *     the scan runs over X_m's predecessors only — the c with R_{c,X_m} > 0,
+ *     increasing c — with fma running sums; first c whose sum reaches U A_m;
+ *     if rounding leaves the sum short, the last predecessor with
+ *     A_{m-1}[c] > 0; if A_m[X_m] <= 0 or no such c: flagged, X_{m-1} = X_m.
  *     The k* virtual event times are uniform order statistics on (0, y),
- *     drawn in decreasing order with the bridge: t_m = t_{m+1} exp(log(U)
- *     invk_m), t_{k*+1} = y.  Self-loops are virtual; a real transition
- *     c -> b at t_m closes b's sojourn (z_b += end - t_m) and counts N[c,b].
- *     Draws per step: U (time), U (state).
+ *     drawn in decreasing order with the bridge in log form:
+ *     l_m = fma(log(U), invk_m, l_{m+1}), l_{k*+1} = 0, t_m = y exp(l_m),
+ *     evaluated only where the path really moves.  Self-loops are virtual;
+ *     a real transition c -> b at t_m closes b's sojourn (z_b += end - t_m)
+ *     and counts N[c,b].  Draws per step: U (time), U (state).
  *  3. Exact: absorbed from j* at y (N[j*,j*]++, the reference's diagonal
  *     convention).  Censored: from j* at y the chain runs forward
  *     (memoryless): sojourn Exp(-S_jj) (two words), Pfull categorical over
@@ -55,9 +61,12 @@ constexpr int kFlagUnifCap = 64;      /* UNIF: Poisson table end, lam cap or zer
 constexpr double kUnifMaxLam = 1300.0; /* w_0 = 2^-1000 keeps every weight finite below this */
 /* kUnifMaxK and unif_tab_doubles: pht_kernels.h (the host sizes the table) */
 
+template <class APtr>
 struct UnifTab {
   const PHT_LDS double *invk, *ax, *ac; /* staged in LDS */
-  const double *A;                      /* global, row k at A + k n */
+  APtr A;                               /* row k at A + k n: LDS when it fits (unif_kernel), else global */
+  const PHT_LDS double *pv;             /* predecessors of b in R: values R_{c,b} at pv[b n + q], */
+  const PHT_LDS int *pc, *np;           /* c at pc[b n + q], q < np[b] (unif_preds) */
   int K;
   double mu, rinv;
 };
@@ -67,8 +76,26 @@ __device__ __forceinline__ double unif_R(const Par<NT> &P, double rinv, int c, i
   return (c == j) ? fma(P.S(c, c), rinv, 1.0) : P.S(c, j) * rinv;
 }
 
-template <int NT, class Sink>
-__device__ __forceinline__ void unif_obs(const Par<NT> &P, const UnifTab &T, double y, int cens, Lane &ln,
+/* b's predecessor list (threads b < n of a block; LDS) */
+template <int NT>
+__device__ __forceinline__ void unif_preds(const Par<NT> &P, double rinv, PHT_LDS double *pv, PHT_LDS int *pc,
+                                           PHT_LDS int *np) {
+  const int n = P.n(), b = threadIdx.x;
+  if (b >= n) return;
+  int q = 0;
+  for (int c = 0; c < n; c++) {
+    const double v = unif_R(P, rinv, c, b);
+    if (v > 0.0) {
+      pv[b * n + q] = v;
+      pc[b * n + q] = c;
+      q++;
+    }
+  }
+  np[b] = q;
+}
+
+template <int NT, class Sink, class APtr>
+__device__ __forceinline__ void unif_obs(const Par<NT> &P, const UnifTab<APtr> &T, double y, int cens, Lane &ln,
                                          Sink &sk) {
   const int n = P.n();
   const double lam = y * T.mu;
@@ -106,7 +133,7 @@ __device__ __forceinline__ void unif_obs(const Par<NT> &P, const UnifTab &T, dou
       w = w * (lam * T.invk[k]);
     }
     const int ks = k;
-    const double *Ak = T.A + (long)ks * n;
+    const APtr Ak = T.A + (long)ks * n;
     const double t2 = dev_u(ln.r) * a[ks];
     double c2 = 0.0;
     js = n - 1;
@@ -119,27 +146,35 @@ __device__ __forceinline__ void unif_obs(const Par<NT> &P, const UnifTab &T, dou
     }
     /* backward bridge */
     b = js;
-    double tm = y, tend = y;
+    double lt = 0.0, tend = y;
     for (int m = ks; m >= 1; m--) {
-      tm = tm * pht_exp_neg(pht_log(dev_u(ln.r)) * T.invk[m]);
-      const double *Am = T.A + (long)(m - 1) * n;
-      double tot = 0.0;
-      for (int c = 0; c < n; c++) tot = fma(Am[c], unif_R(P, T.rinv, c, b), tot);
+      lt = fma(pht_log(dev_u(ln.r)), T.invk[m], lt);
+      const APtr Am = T.A + (long)(m - 1) * n;
+      const double tot = T.A[(long)m * n + b];
       const double tg = dev_u(ln.r) * tot;
-      int cs = b;
+      int cs = -1;
       if (tot > 0.0) {
+        const int np = T.np[b];
+        int last = -1;
         double cum2 = 0.0;
-        for (int c = 0; c < n; c++) {
-          cum2 = fma(Am[c], unif_R(P, T.rinv, c, b), cum2);
+        for (int q = 0; q < np; q++) {
+          const int c = T.pc[b * n + q];
+          const double av = Am[c];
+          cum2 = fma(av, T.pv[b * n + q], cum2);
+          last = (av > 0.0) ? c : last;
           if (cum2 >= tg) {
             cs = c;
             break;
           }
         }
-      } else {
+        if (cs < 0) cs = last;
+      }
+      if (cs < 0) {
         ln.flags |= kFlagUnifCap;
+        cs = b;
       }
       if (cs != b) {
+        const double tm = y * pht_exp_neg(lt);
         sk.z(b, tend - tm);
         sk.N(cs, b);
         ln.njump++;
