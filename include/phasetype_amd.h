@@ -111,8 +111,10 @@ int pht_ctx_rccl_allreduce(pht_ctx *c, long long *buf, int len);
  * (phasetype_amd/csrc/pht_resident.hip), so the host enqueues every sweep
  * and waits once.  Gamma draws come from a counter-based sampler
  * (include/pht_gamma.h), not R's rgamma: the chain is deterministic under
- * set.seed but not the host loop's chain.  Eigen-free samplers only (method
- * 8 UNIF or 1 MHRS, matching the context's method); an attached RCCL
+ * set.seed but not the host loop's chain.  Any method matching the context's
+ * (for ECS/DCS the update also builds the eigensystem, include/pht_eigen.h,
+ * instead of LAPACK: a complex spectrum stops the run with an error, where the
+ * host path warns and uses the real parts as the reference does); an attached RCCL
  * communicator sums every sweep's statistics on the stream (every rank must
  * use the same R-stream seed).  Arguments and res layout as pht_gibbs_run;
  * kernel_ms_total = device time of all sweeps. */

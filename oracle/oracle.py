@@ -121,6 +121,7 @@ class OracleLib:
         L.orc_gibbs_z.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _dp,
                                   _dp, C.c_long, _ip, _dp, _dp, C.c_int]
         L.orc_rgamma_ctr_v.argtypes = [C.c_uint32, C.c_uint32, C.c_double, C.c_double, C.c_long, _dp]
+        L.orc_eig.argtypes = [C.c_int, _dp, _dp, _dp, _dp]
 
     def set_seed(self, seed: int) -> None:
         self.lib.orc_set_seed(seed & 0xFFFFFFFF)
@@ -185,6 +186,16 @@ class OracleLib:
         self.lib.orc_gibbs_z(int(dev), it, mhit, method, n, len(nu), a["nu"], a["zeta"], a["T"], a["C"], a["y"],
                              len(y), a["censored"], a["start"], a["res"], int(zexp))
         return a["res"].reshape(len(nu), it).T.copy()
+
+    def eig(self, S):
+        """The device-resident chain's eigensystem (include/pht_eigen.h):
+        (rc, evals, Q, Qinv), rc 0 = ok, 1 complex pair, 2 no convergence,
+        3 singular eigenvectors."""
+        S = np.asarray(S, np.float64)
+        n = S.shape[0]
+        ev, Q, Qi = np.zeros(n), np.zeros(n * n), np.zeros(n * n)
+        rc = self.lib.orc_eig(n, np.ascontiguousarray(S.reshape(-1, order="F")), ev, Q, Qi)
+        return rc, ev, Q.reshape(n, n, order="F"), Qi.reshape(n, n, order="F")
 
     def rgamma_ctr(self, a, scale, cnt, key=(1, 2)):
         """cnt draws of the device-resident chain's Gamma sampler (include/pht_gamma.h)."""

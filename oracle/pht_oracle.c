@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include "pht_detmath.h"
+#include "pht_eigen.h"
 #include "pht_gamma.h"
 #include "pht_philox.h"
 #include "../phasetype_amd/csrc/rstream.h"
@@ -98,8 +99,18 @@ static int orc_eigen(int n, const double *S, double *evals, double *Q, double *Q
   return info;
 }
 
+/* the resident chain's eigensystem (include/pht_eigen.h, serial here; the
+ * HIP update kernel runs the same loops over one workgroup) */
+int orc_eig(int n, const double *S, double *evals, double *Q, double *Qinv) {
+  static double H[ORC_MAXN * ORC_MAXN], V[ORC_MAXN * ORC_MAXN], X[ORC_MAXN * ORC_MAXN],
+      G[2 * ORC_MAXN * ORC_MAXN], ort[ORC_MAXN], scale[ORC_MAXN], d[ORC_MAXN];
+  pht_eig_ws w = {H, V, X, G, ort, scale, d};
+  return pht_eig(n, S, evals, Q, Qinv, &w);
+}
+
 /* Per-sweep data (src/PHT_MCMC_Aslett.c:279-297, :320-332) + device-mode
- * precomputed products. */
+ * precomputed products.  method | ORC_DEVEIG: the eigensystem by orc_eig
+ * (the device-resident chain) instead of LAPACK. */
 int orc_sp_build(orc_sp *sp, int n, const double *S, const double *s, int method) {
   memset(sp, 0, sizeof *sp);
   sp->n = n;
@@ -121,7 +132,8 @@ int orc_sp_build(orc_sp *sp, int n, const double *S, const double *s, int method
     Pf[i + n * n] = Pf[i + n * n] / rsumfull;
   }
   if (method & (ORC_ECS | ORC_DCS)) {
-    sp->eig_info = orc_eigen(n, S, sp->evals, sp->Q, sp->Qinv);
+    sp->eig_info = (method & ORC_DEVEIG) ? orc_eig(n, S, sp->evals, sp->Q, sp->Qinv)
+                                         : orc_eigen(n, S, sp->evals, sp->Q, sp->Qinv);
     double one[ORC_MAXN];
     for (int i = 0; i < n; i++) one[i] = 1.0;
     orcR_gemv_n(n, sp->Qinv, s, sp->Qinv_s);
@@ -557,7 +569,7 @@ void orc_gibbs_z(int dev, int it, int mhit, int method, int n, int m, const doub
   int disp = dispatch(method);
   for (int iter = 1; iter < it; iter++) {
     if (!disp) continue; /* "CRITICAL ERROR: Unknown sampling method" */
-    orc_sp_build(sp, n, S, s, disp == ORC_MHRS ? ORC_MHRS : method);
+    orc_sp_build(sp, n, S, s, (disp == ORC_MHRS ? ORC_MHRS : method) | (dev == 2 ? ORC_DEVEIG : 0));
     if (!dev) {
       orc_ref_sweep(sp, method, mhit, y, censored, l, z, Bt, Nt, NULL, NULL, NULL, NULL, NULL, NULL, NULL);
     } else {

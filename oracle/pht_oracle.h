@@ -15,6 +15,9 @@
 #define ORC_DCS 0x4
 /* the opt-in uniformisation sampler (no reference counterpart; dev only) */
 #define ORC_UNIF 0x8
+/* orc_sp_build only: the eigensystem by include/pht_eigen.h (the
+ * device-resident chain), not LAPACK */
+#define ORC_DEVEIG 0x100
 
 /* per-sweep data handed to the samplers (src/PHT_MCMC_Aslett.c:276-333).
  * All matrices column-major A[i + j*n]; Pfull is n x (n+1). */

@@ -43,7 +43,7 @@ def needs_build() -> bool:
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps += [os.path.join(REPO, "include", f) for f in ("phasetype_amd.h", "pht_detmath.h", "pht_philox.h",
-                                                          "pht_gamma.h")]
+                                                          "pht_gamma.h", "pht_eigen.h")]
     deps.append(__file__)
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 

@@ -920,6 +920,58 @@ static int unif_prepare(pht_ctx *c, SweepArgs &a) {
   return 0;
 }
 
+/* the sweep kernels of one context on its stream(s): ECS exact and censored
+ * ranges concurrently (stream2 joined back), the other samplers in one
+ * launch; a carries the sweep's common arguments (ctx_enqueue, and the
+ * resident chain per sweep) */
+static int ctx_launch(pht_ctx *c, const SweepArgs &a, bool debug) {
+  if (c->method == kMethodECS) {
+    /* exact observations: persistent ECS kernel; censored: LJMA_samplechain path */
+    SweepArgs ae = a;
+    ae.begin = 0;
+    ae.count = c->n_exact;
+    ae.cens = nullptr;
+    ae.occ = exact_occ(c);
+    ae.rowk = exact_rowk(c);
+    ae.rowprio = getenv("PHT_ROWPRIO") ? atoi(getenv("PHT_ROWPRIO")) : 3;
+    /* lane-major first claims when the shard is within ~2 observations per
+     * lane (the longest paths, one per wavefront; tools/latency.py:
+     * -10 % at 31k-125k per GPU); PHT_SPREAD=0|1 forces it */
+    /* one new observation per lane per round (PHT_NEWCAP=0: no limit;
+     * tools/latency.py: -2 % kernel time at 1e6) */
+    ae.newcap = getenv("PHT_NEWCAP") ? atoi(getenv("PHT_NEWCAP")) : 1;
+    ae.spread = getenv("PHT_SPREAD") ? atoi(getenv("PHT_SPREAD")) : (c->n_exact <= 2 * kSpreadLanes);
+    /* PHT_HOT=k: the remaining-time threshold is the k-th longest exact y */
+    {
+      const long hk = getenv("PHT_HOT") ? atol(getenv("PHT_HOT")) : 0;
+      ae.hoty = (hk > 0 && hk <= c->n_exact) ? c->h_ysorted[hk - 1] : 0.0;
+    }
+    SweepArgs ac = a;
+    ac.begin = c->n_exact;
+    ac.count = c->count - c->n_exact;
+    ac.allcens = 1; /* positions [n_exact, count) hold the censored observations */
+    /* both ranges: the censored kernel on stream2, concurrently, so each
+     * persistent kernel's tail (its longest paths) fills with the other's
+     * work; cfg5 ECS 2.49 -> 1.92 ms; the launch order does not matter
+     * (PHT_CENS_SERIAL=1: one stream) */
+    const bool fork = ae.count > 0 && ac.count > 0 && !getenv("PHT_CENS_SERIAL");
+    if (fork) {
+      HIPCHK(hipEventRecord(c->evf, c->stream));
+      HIPCHK(hipStreamWaitEvent(c->stream2, c->evf, 0));
+      HIPCHK(pht_launch_sweep(&ac, c->method, debug ? 1 : 0, c->stream2));
+      HIPCHK(hipEventRecord(c->evj, c->stream2));
+      HIPCHK(pht_launch_sweep(&ae, c->method, debug ? 1 : 0, c->stream));
+      HIPCHK(hipStreamWaitEvent(c->stream, c->evj, 0));
+    } else {
+      if (ae.count > 0) HIPCHK(pht_launch_sweep(&ae, c->method, debug ? 1 : 0, c->stream));
+      if (ac.count > 0) HIPCHK(pht_launch_sweep(&ac, c->method, debug ? 1 : 0, c->stream));
+    }
+  } else {
+    HIPCHK(pht_launch_sweep(&a, c->method, debug ? 1 : 0, c->stream));
+  }
+  return 0;
+}
+
 static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int zexp, bool debug) {
   HIPCHK(hipSetDevice(c->device));
   const int pb = make_layout(c->n).bytes();
@@ -973,50 +1025,7 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   }
   if (c->method == kMethodUNIF && unif_prepare(c, a)) return -1;
   HIPCHK(hipEventRecord(c->ev0, c->stream));
-  if (c->method == kMethodECS) {
-    /* exact observations: persistent ECS kernel; censored: LJMA_samplechain path */
-    SweepArgs ae = a;
-    ae.begin = 0;
-    ae.count = c->n_exact;
-    ae.cens = nullptr;
-    ae.occ = exact_occ(c);
-    ae.rowk = exact_rowk(c);
-    ae.rowprio = getenv("PHT_ROWPRIO") ? atoi(getenv("PHT_ROWPRIO")) : 3;
-    /* lane-major first claims when the shard is within ~2 observations per
-     * lane (the longest paths, one per wavefront; tools/latency.py:
-     * -10 % at 31k-125k per GPU); PHT_SPREAD=0|1 forces it */
-    /* one new observation per lane per round (PHT_NEWCAP=0: no limit;
-     * tools/latency.py: -2 % kernel time at 1e6) */
-    ae.newcap = getenv("PHT_NEWCAP") ? atoi(getenv("PHT_NEWCAP")) : 1;
-    ae.spread = getenv("PHT_SPREAD") ? atoi(getenv("PHT_SPREAD")) : (c->n_exact <= 2 * kSpreadLanes);
-    /* PHT_HOT=k: the remaining-time threshold is the k-th longest exact y */
-    {
-      const long hk = getenv("PHT_HOT") ? atol(getenv("PHT_HOT")) : 0;
-      ae.hoty = (hk > 0 && hk <= c->n_exact) ? c->h_ysorted[hk - 1] : 0.0;
-    }
-    SweepArgs ac = a;
-    ac.begin = c->n_exact;
-    ac.count = c->count - c->n_exact;
-    ac.allcens = 1; /* positions [n_exact, count) hold the censored observations */
-    /* both ranges: the censored kernel on stream2, concurrently, so each
-     * persistent kernel's tail (its longest paths) fills with the other's
-     * work; cfg5 ECS 2.49 -> 1.92 ms; the launch order does not matter
-     * (PHT_CENS_SERIAL=1: one stream) */
-    const bool fork = ae.count > 0 && ac.count > 0 && !getenv("PHT_CENS_SERIAL");
-    if (fork) {
-      HIPCHK(hipEventRecord(c->evf, c->stream));
-      HIPCHK(hipStreamWaitEvent(c->stream2, c->evf, 0));
-      HIPCHK(pht_launch_sweep(&ac, c->method, debug ? 1 : 0, c->stream2));
-      HIPCHK(hipEventRecord(c->evj, c->stream2));
-      HIPCHK(pht_launch_sweep(&ae, c->method, debug ? 1 : 0, c->stream));
-      HIPCHK(hipStreamWaitEvent(c->stream, c->evj, 0));
-    } else {
-      if (ae.count > 0) HIPCHK(pht_launch_sweep(&ae, c->method, debug ? 1 : 0, c->stream));
-      if (ac.count > 0) HIPCHK(pht_launch_sweep(&ac, c->method, debug ? 1 : 0, c->stream));
-    }
-  } else {
-    HIPCHK(pht_launch_sweep(&a, c->method, debug ? 1 : 0, c->stream));
-  }
+  if (ctx_launch(c, a, debug)) return -1;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   if (c->comm) {
     /* multi-process: the block summed over all ranks in place, on the sweep's
@@ -1445,8 +1454,9 @@ extern "C" int pht_gibbs_run_chains(pht_ctx **ctxs, int nchains, const uint32_t 
  * the optional RCCL all-reduce of the statistics, and resident_update_kernel
  * (pht_resident.hip: conjugate Gamma update by a counter-based sampler, the
  * next sweep's parameter block, the per-sweep checks); the host enqueues all
- * sweeps and waits once.  Eigen-free samplers only (UNIF, MHRS): ECS/DCS need
- * the host's LAPACK eigensystem every sweep.  The chain is a deterministic
+ * sweeps and waits once.  Every sampler: for ECS/DCS the update kernel also
+ * builds the eigensystem (include/pht_eigen.h, one workgroup, in place of the
+ * host's LAPACK dgeevx) and the spectral products.  The chain is a deterministic
  * function of the R stream's two key words (drawn at entry, as
  * pht_gibbs_run does) but NOT the host loop's chain (R's rgamma is replaced).
  */
@@ -1467,9 +1477,9 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
     return -1;
   }
   const int disp = dispatch_method(method);
-  if ((disp != kMethodUNIF && disp != kMethodMHRS) || disp != c->method) {
-    set_err("pht_gibbs_run_resident: the resident chain runs the eigen-free samplers UNIF (8) or MHRS (1), on a "
-            "context created for that method (got method %d, context %d)", method, c->method);
+  if (disp == 0 || disp != c->method) {
+    set_err("pht_gibbs_run_resident: method %d needs a context created for that method (context %d)", method,
+            c->method);
     return -1;
   }
   if (!(ldexp(c->ysum, zexp) < 0x1p62)) {
@@ -1554,6 +1564,7 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
   ra.m = m;
   ra.it = it;
   ra.init = 1;
+  ra.eig = (disp == kMethodECS || disp == kMethodDCS) ? 1 : 0;
   ra.zs = ldexp(1.0, -zexp);
   ra.expect = c->global_count >= 0 ? c->global_count : (c->comm ? -1 : (long long)c->count);
   ra.k0 = k0;
@@ -1629,7 +1640,7 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
   HIPCHK(hipEventRecord(c->ev0, st));
   for (int iter = 1; iter < it; iter++) {
     a.sweep = (uint32_t)iter;
-    if (c->count > 0 || disp == kMethodUNIF) HIPCHK(pht_launch_sweep(&a, disp, 0, st));
+    if ((c->count > 0 || disp == kMethodUNIF) && ctx_launch(c, a, false)) return -1;
     if (c->comm) {
       const ncclResult_t rr =
           rccl().allReduce(c->d_stats, c->d_stats, (size_t)stats_len(n), ncclUint64, ncclSum, c->comm, st);
@@ -1652,9 +1663,11 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
   if (kernel_ms_total) *kernel_ms_total = ms;
   c->flagged = (long long)fl;
   if (err) {
-    set_err("resident chain: %s%s%s", (err & 1) ? "a sweep did not sample every observation; " : "",
+    set_err("resident chain: %s%s%s%s", (err & 1) ? "a sweep did not sample every observation; " : "",
             (err & 2) ? "the fixed-point z sums overflowed (pass a smaller zexp); " : "",
-            (err & 4) ? "a Gamma draw failed (non-finite shape/scale or the rejection cap)" : "");
+            (err & 4) ? "a Gamma draw failed (non-finite shape/scale or the rejection cap); " : "",
+            (err & 8) ? "the eigensystem failed (complex eigenvalues, no QR convergence or singular eigenvectors:"
+                        " the uniformisation sampler, method 8, needs none)" : "");
     return -1;
   }
   if (fl)

@@ -70,6 +70,7 @@ struct SweepArgs {
  * insertion order (the update visits them in reverse, as the host does). */
 struct ResidentArgs {
   int n, m, it, init;
+  int eig;                      /* ECS/DCS: the eigensystem and spectral products too (include/pht_eigen.h) */
   double zs;                    /* 2^-zexp */
   long long expect;             /* observations per sweep, node-wide (< 0: unchecked) */
   uint32_t k0, k1;              /* Philox key of the Gamma streams (include/pht_gamma.h) */
@@ -86,7 +87,7 @@ struct ResidentArgs {
   double *res;                  /* [it * m], res[iter + k it] */
   unsigned char *params;        /* the packed block the next sweep reads */
   unsigned long long *flagged;  /* flagged observation-sweeps, accumulated */
-  int *err;                     /* bit 0: count, bit 1: z overflow, bit 2: Gamma draw */
+  int *err;                     /* bit 0: count, bit 1: z overflow, bit 2: Gamma draw, bit 3: eigensystem */
 };
 
 }  // namespace pht

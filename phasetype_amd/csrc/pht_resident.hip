@@ -9,10 +9,11 @@
  *     conjugate draw Gamma(nu + Nsum, 1 / (zeta + zsum)) — counter-based
  *     (include/pht_gamma.h) instead of R's rgamma — the TT/S/s refresh and
  *     the diagonal in reverse list order;
- *   step 1's setup (src/PHT_MCMC_Aslett.c:279-297): the packed parameter
- *     block of the next sweep (P, Pfull, exit data, candidate lists) with
- *     build_params's arithmetic; no eigensystem (the resident chain runs the
- *     eigen-free samplers: UNIF and MHRS);
+ *   step 1's setup (src/PHT_MCMC_Aslett.c:279-297, :320-332): the packed
+ *     parameter block of the next sweep (P, Pfull, exit data, candidate
+ *     lists) with build_params's arithmetic; for ECS/DCS also the
+ *     eigensystem (include/pht_eigen.h, in place of LAPACK dgeevx) and the
+ *     spectral products;
  *   the checks of the host loop (processed count, z overflow), into an
  *     error word; flagged observations accumulated.
  * init = 1: iteration 0 (GibbsState's constructor: the start row, or the
@@ -21,14 +22,88 @@
 #include <hip/hip_runtime.h>
 
 #include "pht_detmath.h"
+#include "pht_eigen.h"
 #include "pht_gamma.h"
 #include "pht_kernels.h"
 #include "pht_layout.h"
 
 namespace pht {
 
-constexpr int kResThreads = 256;
+/* one wavefront: the eigensolver's phases are separated by barriers, which
+ * cost least within a single wave */
+constexpr int kResThreads = 64;
 constexpr int kResMaxM = (kMaxN + 1) * (kMaxN + 1);
+
+/*
+ * ECS/DCS: the spectral part of build_params (gibbs_host.cpp; the
+ * reference's src/PHT_MCMC_Aslett.c:320-332) from this sweep's S, s, P in
+ * the parameter block: the eigensystem by pht_eig (include/pht_eigen.h) in
+ * place of LAPACK, then Q^-1 s and Q^-1 1 in the reference BLAS dgemv order
+ * and the products QQs, W, QQ1, V, piQ with build_params's fma order.  A
+ * failed eigensystem sets err bit 3 and leaves the previous sweep's spectral
+ * data in place (finite values; the host reports the error after the run);
+ * at init it writes diag(S) and identity vectors instead.
+ */
+__device__ __forceinline__ void spectral(const ResidentArgs &r, int n, const Layout &L, double *dv) {
+  __shared__ double eH[kMaxN * kMaxN], eV[kMaxN * kMaxN], eX[kMaxN * kMaxN], eG[2 * kMaxN * kMaxN];
+  __shared__ double eQ[kMaxN * kMaxN], eort[kMaxN], escale[kMaxN], ed[kMaxN], eev[kMaxN], eQs[kMaxN], eQ1[kMaxN];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  pht_eig_ws w;
+  w.H = eH; w.V = eV; w.X = eX; w.G = eG; w.ort = eort; w.scale = escale; w.d = ed;
+  /* Q^-1 lands in eX (free once the eigenvectors are back-transformed) */
+  const int rc = pht_eig(n, dv + L.S, eev, eQ, eX, &w);
+  __syncthreads();
+  if (rc != PHT_EIG_OK) {
+    if (tid == 0) atomicOr(r.err, 8);
+    if (r.init) {
+      for (int e = tid; e < n * n; e += nt) {
+        const double id = (e % n == e / n) ? 1.0 : 0.0;
+        dv[L.Q + e] = id; dv[L.Qinv + e] = id;
+        dv[L.QQs + e] = id; dv[L.W + e] = id; dv[L.QQ1 + e] = id; dv[L.V + e] = id;
+      }
+      for (int i = tid; i < n; i += nt) {
+        dv[L.evals + i] = dv[L.S + i + i * n];
+        dv[L.piQ + i] = (i == 0) ? 1.0 : 0.0;
+      }
+    }
+    return;
+  }
+  const double *Qi = eX, *s = dv + L.s, *S = dv + L.S, *P = dv + L.P;
+  for (int e = tid; e < n * n; e += nt) {
+    dv[L.Q + e] = eQ[e];
+    dv[L.Qinv + e] = Qi[e];
+  }
+  for (int rr = tid; rr < n; rr += nt) { /* dgemv 'N' order: y = 0; y += x[c] A[:, c] */
+    double qs = 0.0, q1 = 0.0;
+    for (int c = 0; c < n; c++) {
+      const double ts = 1.0 * s[c], t1 = 1.0 * 1.0;
+      qs = qs + ts * Qi[rr + c * n];
+      q1 = q1 + t1 * Qi[rr + c * n];
+    }
+    eQs[rr] = qs;
+    eQ1[rr] = q1;
+    dv[L.evals + rr] = eev[rr];
+  }
+  __syncthreads();
+  for (int e = tid; e < n * n; e += nt) {
+    const int j = e % n, i = e / n;
+    const double Sjj = S[j + j * n];
+    double wv = 0.0, v = 0.0;
+    for (int k = 0; k < n; k++) {
+      if (k != j) wv = fma(S[j + k * n] / (-Sjj), eQ[k + i * n], wv);
+      v = fma(P[j + k * n], eQ[k + i * n], v);
+    }
+    dv[L.QQs + j + i * n] = eQ[j + i * n] * eQs[i];
+    dv[L.W + j + i * n] = wv * eQs[i];
+    dv[L.QQ1 + j + i * n] = eQ[j + i * n] * eQ1[i];
+    dv[L.V + j + i * n] = v * eQ1[i];
+  }
+  for (int i = tid; i < n; i += nt) {
+    double a = 0.0;
+    for (int k = 0; k < n; k++) a = fma(dv[L.pi + k], eQ[k + i * n], a);
+    dv[L.piQ + i] = a;
+  }
+}
 
 __global__ void __launch_bounds__(kResThreads) resident_update_kernel(ResidentArgs r, int iter) {
   __shared__ double theta[kResMaxM];
@@ -147,6 +222,10 @@ __global__ void __launch_bounds__(kResThreads) resident_update_kernel(ResidentAr
     iv[L.nsuccP + j] = a;
     iv[L.nsuccPf + j] = b;
     iv[L.nsuccS + j] = c;
+  }
+  if (r.eig) {
+    __syncthreads();
+    spectral(r, n, L, dv);
   }
   /* the next sweep accumulates into a zeroed block */
   for (int k = tid; k < sl; k += blockDim.x) r.stats[k] = 0ull;

@@ -1,0 +1,67 @@
+"""CPU: the device-resident chain's eigensystem (include/pht_eigen.h, run
+serially by the oracle; the HIP update kernel runs the same loops over one
+workgroup and tests/test_gpu_resident.py checks the two chains bit for bit).
+
+Checked against LAPACK (numpy) — the reference's LJMA_eigen is dgeevx
+(src/utility.c:87-129): eigenvalues to rounding, and the reconstruction
+Q diag(lambda) Q^-1 = S within a small multiple of LAPACK's own error on the
+same matrix (the BD-exit generators' eigenvector matrices are ill-conditioned:
+cond(Q) ~ 5e5 at n = 20).  A complex spectrum is refused (rc 1), where the
+reference warns and uses the real parts (src/utility.c:118-120).
+"""
+import numpy as np
+import pytest
+
+from phasetype_amd.synth import bd_exit
+
+
+def _lapack_err(S):
+    w, V = np.linalg.eig(S)
+    return np.abs(V @ np.diag(w) @ np.linalg.inv(V) - S).max()
+
+
+def _check(orc, S):
+    rc, ev, Q, Qi = orc.eig(S)
+    assert rc == 0
+    w = np.linalg.eigvals(S)
+    assert np.abs(w.imag).max() == 0.0
+    scale = np.abs(w.real).max()
+    assert np.allclose(np.sort(ev), np.sort(w.real), rtol=0, atol=64 * np.finfo(float).eps * scale)
+    err = np.abs(Q @ np.diag(ev) @ Qi - S).max()
+    assert err <= 8 * _lapack_err(S) + 64 * np.finfo(float).eps * scale, (err, _lapack_err(S))
+    assert np.allclose(np.linalg.norm(Q, axis=0), 1.0, rtol=1e-14)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 10, 15, 20, 32])
+def test_eig_bd_exit(orc, n):
+    S, _ = bd_exit(n)
+    _check(orc, S)
+
+
+@pytest.mark.parametrize("n,seed", [(4, 0), (8, 1), (12, 2), (20, 3), (20, 4)])
+def test_eig_random_tridiagonal_generators(orc, n, seed):
+    """Birth-death sub-generators with random rates over three decades (real
+    spectrum: similar to a symmetric matrix); balancing matters here."""
+    rng = np.random.default_rng(seed)
+    up, dn = 10.0 ** rng.uniform(-1.5, 1.5, n - 1), 10.0 ** rng.uniform(-1.5, 1.5, n - 1)
+    S = np.diag(up, 1) + np.diag(dn, -1)
+    s = 10.0 ** rng.uniform(-2, 0, n)
+    S[np.diag_indices(n)] = -(S.sum(1) + s)
+    _check(orc, S)
+
+
+@pytest.mark.parametrize("n,seed", [(5, 5), (10, 6), (16, 7)])
+def test_eig_random_triangular_generators(orc, n, seed):
+    """Acyclic (upper-triangular) sub-generators, e.g. Coxian: the spectrum is
+    the diagonal; distinct rates."""
+    rng = np.random.default_rng(seed)
+    S = np.triu(rng.exponential(1.0, (n, n)) * (rng.random((n, n)) < 0.6), 1)
+    s = rng.exponential(0.5, n)
+    S[np.diag_indices(n)] = -(S.sum(1) + s) - np.arange(n) * 0.37
+    _check(orc, S)
+
+
+def test_eig_complex_spectrum_refused(orc):
+    S = np.array([[-10.1, 10.0, 0.0], [0.0, -10.1, 10.0], [10.0, 0.0, -10.1]])
+    rc, *_ = orc.eig(S)
+    assert rc == 1

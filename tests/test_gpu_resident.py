@@ -3,13 +3,15 @@
 blocks all on the device, one host wait per run.
 
 * bit for bit against the oracle's restatement of the same chain (oracle
-  gibbs dev=2: the GPU spec's sweeps + include/pht_gamma.h draws), UNIF and
-  MHRS, with censoring;
+  gibbs dev=2: the GPU spec's sweeps + include/pht_gamma.h draws +
+  include/pht_eigen.h's eigensystem for ECS/DCS), every sampler, with
+  censoring;
 * in distribution against the reference: posterior means and quantiles
-  within 5 combined MCSEs of tests/golden/g5_posterior.npz (UNIF against the
-  reference's ECS chains — the same conditional path law — and MHRS against
-  the reference's MHRS chains);
-* the guards: eigen-based samplers refused, the processed-count check.
+  within 5 combined MCSEs of tests/golden/g5_posterior.npz (ECS, DCS and
+  MHRS against the reference's chains of the same sampler; UNIF against the
+  reference's ECS chains — the same conditional path law);
+* the guards: a method other than the context's, a complex spectrum (the
+  device eigensystem stops the run), the processed-count check.
 """
 import os
 
@@ -26,7 +28,8 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "g5_po
 
 
 @pytest.mark.parametrize("method,n,mhit,cf", [(8, 6, 1, 0.3), (8, 10, 1, 0.0), (1, 4, 1, 0.3), (1, 4, 3, 0.0),
-                                              (8, 15, 1, 0.3)])
+                                              (8, 15, 1, 0.3), (2, 3, 1, 0.0), (2, 6, 1, 0.3), (2, 10, 1, 0.0),
+                                              (2, 20, 1, 0.0), (4, 5, 1, 0.3), (4, 10, 1, 0.0)])
 def test_resident_chain_bitexact(gpu, orc, method, n, mhit, cf):
     T, theta = bd_exit_structure(n)
     S, s = bd_exit(n)
@@ -69,7 +72,8 @@ def test_resident_start_and_small_prior_shapes(gpu, orc):
 
 
 @pytest.mark.parametrize("name,method", [("n10_ecs", 8), ("n15_cens_ecs", 8), ("n20_ecs", 8), ("cfg1_mhrs", 1),
-                                         ("n15_cens_mhrs", 1)])
+                                         ("n15_cens_mhrs", 1), ("cfg1_ecs", 2), ("n10_ecs", 2),
+                                         ("n15_cens_ecs", 2), ("n15_cens_dcs", 4)])
 def test_resident_chain_matches_reference_posterior(gpu, name, method):
     n, _, mhit, y, cen, T, nu, zeta = PO.case_inputs(name)
     ref = PO.unpack(np.load(GOLD), name)
@@ -92,8 +96,18 @@ def test_resident_guards(gpu):
     nu, zeta, Cm = 1 + 50 * theta, np.full(m, 50.0), np.ones(T.shape)
     sw = P.Sweeper(n, 2, 1)
     sw.set_obs(y, cen)
-    with pytest.raises(P.PhaseTypeError, match="eigen-free"):
-        sw.gibbs_resident(5, 2, nu, zeta, T, Cm, P.zexp_for(y))
+    with pytest.raises(P.PhaseTypeError, match="context created for that method"):
+        sw.gibbs_resident(5, 8, nu, zeta, T, Cm, P.zexp_for(y))
+    sw.close()
+    # a 3-cycle with weak exits: complex eigenvalues, the device eigensystem
+    # stops the chain (the host path warns and uses the real parts)
+    Tc = np.zeros((4, 4), np.int32)
+    Tc[0, 1], Tc[1, 2], Tc[2, 0], Tc[0, 3], Tc[1, 3], Tc[2, 3] = 1, 1, 1, 2, 2, 2
+    yc = np.random.default_rng(2).exponential(3.0, 500)
+    sw = P.Sweeper(3, 2, 1)
+    sw.set_obs(yc, np.zeros(500, np.int32))
+    with pytest.raises(P.PhaseTypeError, match="eigensystem failed"):
+        sw.gibbs_resident(4, 2, np.array([501.0, 6.0]), np.array([50.0, 50.0]), Tc, np.ones((4, 4)), P.zexp_for(yc))
     sw.close()
     sw = P.Sweeper(n, 8, 1)
     sw.set_obs(y, cen)

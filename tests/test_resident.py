@@ -4,9 +4,10 @@ opt-in, non-parity).
 * The counter-based Gamma sampler (include/pht_gamma.h, shared by the HIP
   update kernel and the oracle) against scipy's Gamma law: Kolmogorov-
   Smirnov over shapes from 0.3 (the a < 1 boost) to 10^5, and the scale.
-* The resident chain (oracle gibbs dev=2: UNIF sweeps, device Gamma update)
-  against the reference ECS posterior of cfg1 (oracle/posterior.py): same
-  data and priors, within 5 combined MCSEs.
+* The resident chain (oracle gibbs dev=2: device Gamma update; UNIF sweeps,
+  and ECS sweeps on the resident eigensystem) against the reference ECS
+  posterior of cfg1 (oracle/posterior.py): same data and priors, within 5
+  combined MCSEs.
 GPU: tests/test_gpu_resident.py (bit-exact with this oracle chain)."""
 import os
 
@@ -34,10 +35,11 @@ def test_counter_gamma_is_deterministic_and_keyed(orc):
     assert not np.array_equal(a, orc.rgamma_ctr(3.0, 1.0, 100, key=(1, 3)))
 
 
-@pytest.mark.parametrize("name", ["cfg1_ecs"])
-def test_resident_unif_chain_matches_reference_posterior(orc, name):
-    n, method, mhit, y, cen, T, nu, zeta = PO.case_inputs(name)
+@pytest.mark.parametrize("name,method", [("cfg1_ecs", 8), ("cfg1_ecs", 2)])
+def test_resident_chain_matches_reference_posterior(orc, name, method):
+    """UNIF, and ECS with the resident eigensystem (include/pht_eigen.h)."""
+    n, _, mhit, y, cen, T, nu, zeta = PO.case_inputs(name)
     orc.set_seed(5)
-    chain = orc.gibbs(2, 3001, 1, 8, n, nu, zeta, T.reshape(-1, order="F"), np.ones(T.size), y, cen)
+    chain = orc.gibbs(2, 3001, 1, method, n, nu, zeta, T.reshape(-1, order="F"), np.ones(T.size), y, cen)
     ok, worst, bad = PO.compare(PO.summarize(chain), PO.unpack(np.load(GOLD), name))
     assert ok, (worst, bad[:5])

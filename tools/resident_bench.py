@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Sweeps/s of the device-resident chain (pht_gibbs_run_resident, UNIF and
-MHRS) next to the host-loop chain (pht_gibbs_run) with the same sampler, and
-the host-loop ECS chain, at BASELINE.json's single-GPU configurations.
+"""Sweeps/s of the device-resident chain (pht_gibbs_run_resident) next to
+the host-loop chain (pht_gibbs_run) with the same sampler (ECS, DCS at cfg5,
+UNIF, MHRS), at BASELINE.json's single-GPU configurations; argv: config
+names and/or methods to restrict to.
 Prints one JSON line per (config, mode).  Run on the GPU box."""
 import json
 import os
@@ -18,15 +19,17 @@ CFGS = [("cfg1", 3, 200, 0.0, 2000), ("cfg2", 5, 10_000, 0.0, 1000), ("cfg3", 20
         ("cfg4", 10, 1_000_000, 0.0, 100), ("cfg5", 15, 500_000, 0.3, 100)]
 want = set(sys.argv[1:])
 for name, n, N, cf, steps in CFGS:
-    if want and name not in want:
+    if want - set(P.METHODS) and name not in want:
         continue
     S, s = bd_exit(n)
     T, theta = bd_exit_structure(n)
     nu, zeta, Cm = 1 + 50 * theta, np.full(len(theta), 50.0), np.ones(T.shape)
     y, cen = simulate_ph(S, s, N, seed=DATA_KEY, censor_frac=cf)
     zexp = P.zexp_for(y)
-    for meth, mode in (("ECS", "host"), ("UNIF", "host"), ("UNIF", "resident"), ("MHRS", "host"),
-                       ("MHRS", "resident")):
+    meths = ["ECS", "UNIF", "MHRS"] + (["DCS"] if cf > 0 else [])
+    for meth, mode in [(m, md) for m in meths for md in ("host", "resident")]:
+        if want & set(P.METHODS) and meth not in want:
+            continue
         mm = P.METHODS[meth]
         sw = P.Sweeper(n, mm, 1)
         sw.set_obs(y, cen)
