@@ -122,6 +122,7 @@ class OracleLib:
                                   _dp, C.c_long, _ip, _dp, _dp, C.c_int]
         L.orc_rgamma_ctr_v.argtypes = [C.c_uint32, C.c_uint32, C.c_double, C.c_double, C.c_long, _dp]
         L.orc_eig.argtypes = [C.c_int, _dp, _dp, _dp, _dp]
+        L.orc_set_dcs_brent.argtypes = [C.c_int]
 
     def set_seed(self, seed: int) -> None:
         self.lib.orc_set_seed(seed & 0xFFFFFFFF)
@@ -186,6 +187,11 @@ class OracleLib:
         self.lib.orc_gibbs_z(int(dev), it, mhit, method, n, len(nu), a["nu"], a["zeta"], a["T"], a["C"], a["y"],
                              len(y), a["censored"], a["start"], a["res"], int(zexp))
         return a["res"].reshape(len(nu), it).T.copy()
+
+    def set_dcs_brent(self, on: bool) -> None:
+        """dev variant's DCS root finder: Find02's Brent search (on) or the
+        device spec's default safeguarded Halley iteration (off)."""
+        self.lib.orc_set_dcs_brent(1 if on else 0)
 
     def eig(self, S):
         """The device-resident chain's eigensystem (include/pht_eigen.h):

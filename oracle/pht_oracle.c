@@ -34,6 +34,11 @@ double orc_rgamma(double a, double scale) { return pht_rs_rgamma(&g_rs, a, scale
 double orc_exp_rand(void) { return pht_rs_exp_rand(&g_rs); }
 double orc_norm_rand(void) { return pht_rs_norm_rand(&g_rs); }
 
+/* dev variant's DCS jump-time root finder: 0 = hob_halley (the device
+ * spec's default), 1 = Find02 (PHT_DCS_ROOT=brent on the device) */
+static int orc_dcs_brent = 0;
+void orc_set_dcs_brent(int on) { orc_dcs_brent = on; }
+
 /* ------------------------------------------------------------ variants */
 #define ORC_DEV 0
 #define ORC_FN(x) orcR_##x

@@ -944,6 +944,63 @@ static double ORC_FN(find02)(double ax, double bx, double fa, double fb, orc_den
   return b;
 }
 
+#if ORC_DEV
+/* the device spec's jump-time root (pht_dcs_round.h hob_halley): safeguarded
+ * Halley on HobCDF, F' and F'' from the same exponentials, stop at the
+ * evaluation's rounding level; E, Qb, coef as the kernel hoists them.
+ * Evaluations counted into *nev. */
+static double ORC_FN(hob_halley)(const ORC_FN(hob_ctx) *c, double es, int *nev) {
+  const orc_sp *sp = c->sp;
+  const int n = sp->n;
+  const double eps = 2.2204460492503131e-16;
+  const double Sll = sp->S[c->lastj + c->lastj * n];
+  const double X = c->y - c->t;
+  const double coef = 1 / c->prob * sp->S[c->lastj + c->j * n] / c->Pab;
+  double lo = 0.0, hi = X;
+  const double x0 = ORC_LOG(1.0 - c->u * (1.0 - es)) / Sll;
+  double xb = (x0 > lo && x0 < hi) ? x0 : c->u * X;
+  double root = xb;
+  for (int it = 0; it < 1000; it++) {
+    const double c1 = X - xb, c0 = Sll * xb;
+    double tmp = 0.0, asum = 0.0, dtmp = 0.0, d2 = 0.0;
+    for (int i = 0; i < n; i++) {
+      const double Ei = c->E[i], ev = sp->evals[i];
+      double ei, Ji, dl;
+      if (fabs((ev - Sll) / Sll) < 1e-13) {
+        ei = Ei;
+        Ji = xb * Ei;
+        dl = 0.0;
+      } else {
+        ei = ORC_EXP_NEG(c1 * ev + c0);
+        Ji = (Ei - ei) * (1.0 / (ev - Sll));
+        dl = Sll - ev;
+      }
+      const double q = sp->Q[c->j + i * n], qb = c->Qb[i];
+      const double qJ = q * Ji, qe = q * ei;
+      tmp = fma(qJ, qb, tmp);
+      asum = fma(fabs(qJ), fabs(qb), asum);
+      dtmp = fma(qe, qb, dtmp);
+      d2 = fma(qe * dl, qb, d2);
+    }
+    (*nev)++;
+    const double F = coef * tmp - c->u, D = coef * dtmp, D2 = coef * d2;
+    if (F == 0.0) { root = xb; break; }
+    if (F < 0.0) lo = xb;
+    else hi = xb;
+    double nx = xb - (2.0 * F * D) / (2.0 * D * D - F * D2);
+    if (fabs(F) <= 16.0 * eps * (coef * asum + c->u)) {
+      root = (nx >= lo && nx <= hi) ? nx : xb;
+      break;
+    }
+    if (!(nx > lo && nx < hi)) nx = 0.5 * (lo + hi);
+    root = nx;
+    if (fabs(nx - xb) <= 2.0 * eps * fabs(xb)) break;
+    xb = nx;
+  }
+  return root;
+}
+#endif
+
 /* LJMA_Hobolth_endState + LJMA_samplechain_Hobolth, one observation
  * (censoring ignored, as the reference: :132). */
 static void ORC_FN(obs_dcs)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_obs *o, double zscale,
@@ -1058,10 +1115,19 @@ static void ORC_FN(obs_dcs)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_ob
     hc.E = E;
 #endif
     hc.u = ORC_FN(runif)(rng, 0.0, 1.0);
-    double Tol = 0.0;
-    int Maxit = 1000;
-    jtime = ORC_FN(find02)(0.0, y - t, -hc.u, 1.0 - hc.u, ORC_FN(hobcdf), &hc, &Tol, &Maxit);
-    if (nbrent) *nbrent += (Maxit < 0) ? 1000 : Maxit;
+#if ORC_DEV
+    if (!orc_dcs_brent) {
+      int nev = 0;
+      jtime = ORC_FN(hob_halley)(&hc, ORC_EXP_NEG(Sjj * x), &nev);
+      if (nbrent) *nbrent += nev;
+    } else
+#endif
+    {
+      double Tol = 0.0;
+      int Maxit = 1000;
+      jtime = ORC_FN(find02)(0.0, y - t, -hc.u, 1.0 - hc.u, ORC_FN(hobcdf), &hc, &Tol, &Maxit);
+      if (nbrent) *nbrent += (Maxit < 0) ? 1000 : Maxit;
+    }
     while (t + jtime >= y) jtime = jtime / 2;
     o->N[lastj + j * n]++;
     ORC_FN(zadd)(o, lastj, jtime, zscale);

@@ -525,6 +525,7 @@ static void group_fire(ChainGroup *g) {
 }
 
 static int unif_prepare(pht_ctx *c, SweepArgs &a);
+static int dcs_brent();
 
 /* chain c's sweep (parameters in c->h_params): returns when the group's sweep
  * is done, with c->h_stats and c->last_ms filled */
@@ -544,6 +545,7 @@ static int group_sweep(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   a.k1 = k1;
   a.sweep = sweep;
   a.zscale = ldexp(1.0, zexp);
+  a.dcsbrent = dcs_brent();
   a.stats = ds;
   SweepArgs ae = a, ac = a;
   if (g->method == kMethodECS) {
@@ -920,6 +922,14 @@ static int unif_prepare(pht_ctx *c, SweepArgs &a) {
   return 0;
 }
 
+/* DCS jump-time root finder: PHT_DCS_ROOT=brent selects the reference's
+ * Find02 search (src/utility.c:233-338) over the default safeguarded Halley
+ * iteration (pht_dcs_round.h hob_halley); read per sweep */
+static int dcs_brent() {
+  const char *e = getenv("PHT_DCS_ROOT");
+  return (e && !strcmp(e, "brent")) ? 1 : 0;
+}
+
 /* the sweep kernels of one context on its stream(s): ECS exact and censored
  * ranges concurrently (stream2 joined back), the other samplers in one
  * launch; a carries the sweep's common arguments (ctx_enqueue, and the
@@ -996,6 +1006,7 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   a.k1 = k1;
   a.sweep = sweep;
   a.zscale = ldexp(1.0, zexp);
+  a.dcsbrent = dcs_brent();
   a.stats = c->d_stats;
   a.mbest = c->d_mbest;
   a.mq0 = c->d_mq0;
@@ -1603,6 +1614,7 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
   a.k0 = k0;
   a.k1 = k1;
   a.zscale = ldexp(1.0, zexp);
+  a.dcsbrent = dcs_brent();
   a.stats = c->d_stats;
   a.mbest = c->d_mbest;
   a.mq0 = c->d_mq0;

@@ -45,6 +45,7 @@ struct SweepArgs {
                                   blocks (both set by the launcher) */
   int nmain;
   int rowprio;                 /* ECS exact: wave priority of the row blocks (s_setprio 0-3) */
+  int dcsbrent;                /* DCS: jump times by Find02's Brent search instead of hob_halley (pht_dcs_round.h) */
   /* MHRS attempt search (pht_kernels.hip, MHRS section): per chain task
    * (position * (1 + mhit) + c) its first success (attempt << 8 | pre), two
    * task queues and the queue counters; allocated by the host for MHRS */

@@ -64,6 +64,38 @@ def test_per_observation_bitexact(gpu, orc, n, N, cf, method, mhit):
     assert np.array_equal(st[:2 * n + n * n], g["stats"][:2 * n + n * n])
 
 
+@pytest.mark.parametrize("n,N,cf", [(3, 2000, 0.0), (10, 1000, 0.3), (15, 300, 0.0)])
+def test_dcs_brent_root_bitexact(gpu, orc, monkeypatch, n, N, cf):
+    """PHT_DCS_ROOT=brent: the jump times by Find02's Brent search (the
+    reference's root finder) instead of the default Halley iteration, GPU vs
+    the oracle's device spec in the same mode, bit for bit; and the default
+    mode lands on the same discrete path with z equal to rounding."""
+    S0, s0 = bd_exit(n)
+    y, cen = simulate_ph(S0, s0, N, seed=2000 + n, censor_frac=cf)
+    S, s = _perturbed(n, n + 1)
+    key, sweep = (0x777 + n, 0x31), 3
+    zexp = int(orc.lib.orc_zexp(np.ascontiguousarray(y), len(y)))
+    monkeypatch.setenv("PHT_DCS_ROOT", "brent")
+    orc.set_dcs_brent(True)
+    try:
+        o = orc.dev_sweep(4, S, s, y, cen, key=key, sweep=sweep, zexp=zexp)
+    finally:
+        orc.set_dcs_brent(False)
+    sw = P.Sweeper(n, 4, 1)
+    sw.set_obs(y, cen)
+    g = sw.sweep_debug(S, s, key=key, sweep=sweep, zexp=zexp)
+    for f in ("B", "pre", "flags", "ndraw", "zq", "N"):
+        assert np.array_equal(g[f], o[f]), f
+    monkeypatch.delenv("PHT_DCS_ROOT")
+    h = sw.sweep_debug(S, s, key=key, sweep=sweep, zexp=zexp)
+    sw.close()
+    for f in ("B", "pre", "N", "ndraw"):
+        assert np.array_equal(h[f], g[f]), f
+    assert np.abs(h["zq"] - g["zq"]).max() <= 1e-9 * np.abs(g["zq"]).max()
+    # Brent's evaluations (stats word 5) against the Halley iteration's
+    assert P.split_stats(h["stats"], n)[3][5] * 2 < P.split_stats(g["stats"], n)[3][5]
+
+
 @pytest.mark.parametrize("method", [1, 2, 4])
 def test_shard_invariance(gpu, method):
     """Two shards (obs0 offsets) sum to the single-shard block exactly."""
