@@ -125,9 +125,32 @@ __device__ __forceinline__ void brent_tail(BrentSt &s, double fb) {
  * root agrees with Find02's to the evaluation's rounding (~1e-12 relative);
  * ~3.8 evaluations per jump at n = 3..20 (p90 4) where Find02 takes ~11.
  */
-constexpr int kDcsRootMax = 1000;
+/* a lane's e^{lambda_i (y - t)}: registers for small n, lane-interleaved
+ * LDS rows from n = 10 (and the runtime-n kernel), where registers spilled
+ * (n = 15 / 20 kernel -13 % / -14 %, n = 5 +4 % in LDS) */
 template <int NT>
-__device__ __forceinline__ double hob_halley(const Par<NT> &P, const double *E, const PHT_LDS double *rv, unsigned near,
+constexpr bool dcs_e_in_lds() { return NT == 0 || NT >= 10; }
+template <int NT, bool LDS = dcs_e_in_lds<NT>()>
+struct DcsE {
+  double v[PHT_VEC(NT)];
+  __device__ __forceinline__ double get(int i) const { return v[i]; }
+  __device__ __forceinline__ void set(int i, double x) { v[i] = x; }
+};
+template <int NT>
+struct DcsE<NT, true> {
+  PHT_LDS double *p; /* this lane's column: E(i) at p[i kBlock] */
+  __device__ __forceinline__ double get(int i) const { return p[i * kBlock]; }
+  __device__ __forceinline__ void set(int i, double x) { p[i * kBlock] = x; }
+};
+
+constexpr int kDcsRootMax = 1000;
+/* in the unrolled n-term loops of the n >= 10 kernels: keep the scheduler
+ * from interleaving more than 4 exponentials at once (each holds ~6 double
+ * temporaries; 15 in flight spilled the n = 15 kernel) */
+#define PHT_DCS_CHUNK(i) \
+  if (dcs_e_in_lds<NT>() && ((i) & 3) == 3) __builtin_amdgcn_sched_barrier(0)
+template <int NT>
+__device__ __forceinline__ double hob_halley(const Par<NT> &P, const DcsE<NT> &E, const PHT_LDS double *rv, unsigned near,
                                              double Sjj, double X, double es, double coef, double u, int jn, int b,
                                              Lane &ln) {
   const int n = P.n();
@@ -141,7 +164,7 @@ __device__ __forceinline__ double hob_halley(const Par<NT> &P, const double *E, 
     double tmp = 0.0, asum = 0.0, dtmp = 0.0, d2 = 0.0;
 #pragma unroll
     for (int i = 0; i < n; i++) {
-      const double Ei = E[i], ev = P.evals(i);
+      const double Ei = E.get(i), ev = P.evals(i);
       double ei, Ji, dl;
       if ((near >> i) & 1u) {
         ei = Ei;
@@ -158,6 +181,7 @@ __device__ __forceinline__ double hob_halley(const Par<NT> &P, const double *E, 
       asum = fma(fabs(qJ), fabs(qb), asum);
       dtmp = fma(qe, qb, dtmp);
       d2 = fma(qe * dl, qb, d2);
+      PHT_DCS_CHUNK(i);
     }
     ln.nbrent++;
     const double F = coef * tmp - u, D = coef * dtmp, D2 = coef * d2;
@@ -185,7 +209,12 @@ __device__ __forceinline__ double hob_halley(const Par<NT> &P, const double *E, 
 __host__ __device__ constexpr int dcs_rinv_offset(int pbytes, int n) {
   return (pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 4 * n + 7) & ~7;
 }
-__host__ __device__ constexpr int dcs_smem_bytes(int pbytes, int n) { return dcs_rinv_offset(pbytes, n) + 8 * n * n; }
+/* then each lane's e^{lambda_i (y - t)} of the current jump, lane-interleaved
+ * (E(i) at [i kBlock + lane]): in registers they pushed the n = 10..20
+ * kernels past 256 VGPRs (n = 15: 202 spilled, ~2.4 GB of scratch traffic
+ * per cfg5 sweep) */
+__host__ __device__ constexpr int dcs_e_offset(int pbytes, int n) { return dcs_rinv_offset(pbytes, n) + 8 * n * n; }
+__host__ __device__ constexpr int dcs_smem_bytes(int pbytes, int n) { return dcs_e_offset(pbytes, n) + 8 * n * kBlock; }
 
 /* per-lane path state between jumps */
 struct DcsLane {
@@ -219,6 +248,8 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
   /* rinv[j n + i] = 1 / (lambda_i - S_jj): J's divisor as a reciprocal
    * (device spec) */
   PHT_LDS double *rinv = (PHT_LDS double *)(lsm + dcs_rinv_offset(pbytes, n));
+  DcsE<NT> e;
+  if constexpr (dcs_e_in_lds<NT>()) e.p = (PHT_LDS double *)(lsm + dcs_e_offset(pbytes, n)) + threadIdx.x;
   pht_stage_math_tables();
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
@@ -290,12 +321,12 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
   /* a new observation's end state ~ (pi e^{yS})_b s_b (endState,
    * src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:11-51) from its
    * e^{lambda_i y}, start state, and the jump loop's head */
-  auto new_obs = [&](const double *ey) {
+  auto new_obs = [&](const DcsE<NT> &ey) {
     /* (the weights are recomputed in the scan, as dcs() does, instead of
      * held in registers) */
     double av[PHT_VEC(NT)];
 #pragma unroll
-    for (int i = 0; i < n; i++) av[i] = P.piQ(i) * ey[i];
+    for (int i = 0; i < n; i++) av[i] = P.piQ(i) * ey.get(i);
     double sum = 0.0;
 #pragma unroll 1
     for (int k = 0; k < n; k++) {
@@ -373,11 +404,13 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
 
     /* ---- e^{lambda_i (y - t)} for every lane (converged): this jump's E,
      * and for a new observation (t = 0) also its end-state vector */
-    double e[PHT_VEC(NT)];
     if (act) {
       const double x = st.y - st.t;
 #pragma unroll
-      for (int i = 0; i < n; i++) e[i] = pht_exp_neg(P.evals(i) * x);
+      for (int i = 0; i < n; i++) {
+        e.set(i, pht_exp_neg(P.evals(i) * x));
+        PHT_DCS_CHUNK(i);
+      }
     }
 
     /* ---- a new observation: end state ~ (pi e^{yS})_b s_b (endState,
@@ -391,10 +424,10 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
       const double x = st.y - st.t;
       const double Sjj = P.S(j, j);
       const unsigned near = nearm[j];
-      const double *E = e; /* this jump's e^{lambda_i x} */
+      const DcsE<NT> &E = e; /* this jump's e^{lambda_i x} */
       double Pab = 0.0;
 #pragma unroll
-      for (int i = 0; i < n; i++) Pab = fma(P.Q(j, i) * E[i], P.Qinv(i, st.b), Pab);
+      for (int i = 0; i < n; i++) Pab = fma(P.Q(j, i) * E.get(i), P.Qinv(i, st.b), Pab);
       bool done = false;
       if (j == st.b) {
         if (dev_runif(ln.r, 0.0, 1.0) < pht_exp_neg(Sjj * (st.y - st.t)) / Pab) {
@@ -410,19 +443,23 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
         const double es = pht_exp_neg(Sjj * x);
 #pragma unroll
         for (int i = 0; i < n; i++) {
-          if ((near >> i) & 1u) J[i] = x * E[i];
-          else J[i] = (E[i] - es) * rinv[j * n + i];
+          if ((near >> i) & 1u) J[i] = x * E.get(i);
+          else J[i] = (E.get(i) - es) * rinv[j * n + i];
         }
         const int cnt = P.nsuccS(j);
-        double pw[PHT_VEC(NT)];
-        double p_sum = 0.0;
-        for (int q = 0; q < cnt; q++) {
+        /* successor weights S_ji / Pab * (Q J Qb)_i: summed here, then
+         * recomputed (same operations, same values) in the scan below, so no
+         * per-lane array indexed by the runtime successor count lands in
+         * scratch */
+        auto weight = [&](int q) {
           const int i = P.succS(j, q);
           double tmp = 0.0;
 #pragma unroll
           for (int k = 0; k < n; k++) tmp = fma(P.Q(i, k) * J[k], P.Qinv(k, st.b), tmp);
-          p_sum += pw[q] = P.S(j, i) / Pab * tmp;
-        }
+          return P.S(j, i) / Pab * tmp;
+        };
+        double p_sum = 0.0;
+        for (int q = 0; q < cnt; q++) p_sum += weight(q);
         const double target = dev_runif(ln.r, 0.0, p_sum);
         if (!(target > 0.0)) {
           ln.flags |= kFlagDcsZero;
@@ -430,18 +467,18 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
           finish_obs();
           done = true;
         } else {
-          double sofar = 0.0;
+          double sofar = 0.0, prob = 0.0;
           int q = 0;
           for (; q < cnt; q++) {
-            sofar += pw[q];
+            prob = weight(q);
+            sofar += prob;
             if (!(sofar < target)) break;
           }
-          if (q == cnt) {
+          if (q == cnt) { /* prob is the last successor's weight */
             ln.flags |= kFlagScanEnd;
             q = cnt - 1;
           }
           st.j = P.succS(j, q);
-          const double prob = pw[q];
           /* HobCDF (src/Simulate_AbsCTMC_gt_Hobolth_DCS.c:23-47):
            * 1/prob * S_{lastj,j} / Pab * sum_i Q_ji J_i(x) Qb_i - u, its
            * factor hoisted out of the evaluations (same operations) */
@@ -475,11 +512,12 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
               double tmp = 0.0;
 #pragma unroll
               for (int i = 0; i < n; i++) {
-                const double ev = P.evals(i), Ei = E[i];
+                const double ev = P.evals(i), Ei = E.get(i);
                 double Ji;
                 if ((near >> i) & 1u) Ji = xb * Ei;
                 else Ji = (Ei - pht_exp_neg(c1 * ev + c0)) * rinv[j * n + i];
                 tmp = fma(P.Q(jn, i) * Ji, P.Qinv(i, st.b), tmp);
+                PHT_DCS_CHUNK(i);
               }
               ln.nbrent++;
               brent_tail(bs, coef * tmp - u);
