@@ -126,10 +126,13 @@ __device__ __forceinline__ void brent_tail(BrentSt &s, double fb) {
  * ~3.8 evaluations per jump at n = 3..20 (p90 4) where Find02 takes ~11.
  */
 /* a lane's e^{lambda_i (y - t)}: registers for small n, lane-interleaved
- * LDS rows from n = 10 (and the runtime-n kernel), where registers spilled
+ * LDS rows from n = 10, where registers spilled
  * (n = 15 / 20 kernel -13 % / -14 %, n = 5 +4 % in LDS) */
+/* where the E rows live (compile-time n >= 10: at most 20 rows; the
+ * runtime-n kernel keeps E in registers, its n <= 32 rows would not fit
+ * beside a 32-state parameter block) */
 template <int NT>
-constexpr bool dcs_e_in_lds() { return NT == 0 || NT >= 10; }
+constexpr bool dcs_e_in_lds() { return NT >= 10; }
 template <int NT, bool LDS = dcs_e_in_lds<NT>()>
 struct DcsE {
   double v[PHT_VEC(NT)];
@@ -214,7 +217,10 @@ __host__ __device__ constexpr int dcs_rinv_offset(int pbytes, int n) {
  * kernels past 256 VGPRs (n = 15: 202 spilled, ~2.4 GB of scratch traffic
  * per cfg5 sweep) */
 __host__ __device__ constexpr int dcs_e_offset(int pbytes, int n) { return dcs_rinv_offset(pbytes, n) + 8 * n * n; }
-__host__ __device__ constexpr int dcs_smem_bytes(int pbytes, int n) { return dcs_e_offset(pbytes, n) + 8 * n * kBlock; }
+template <int NT>
+constexpr int dcs_smem_bytes(int pbytes, int n) {
+  return dcs_e_offset(pbytes, n) + (dcs_e_in_lds<NT>() ? 8 * n * kBlock : 0);
+}
 
 /* per-lane path state between jumps */
 struct DcsLane {

@@ -1076,7 +1076,7 @@ dcs_round_kernel(SweepArgs a) {
 template <int NT, bool DEBUG>
 static hipError_t launch_dcs_round(const SweepArgs &a, hipStream_t st) {
   static LaunchCfg cfg;
-  const int sm = dcs_smem_bytes(make_layout(a.n).bytes(), a.n); /* + near masks, reciprocals */
+  const int sm = dcs_smem_bytes<NT>(make_layout(a.n).bytes(), a.n); /* + near masks, reciprocals */
   int occ = 0, cus = 0;
   if (hipError_t e = launch_config(cfg, (const void *)dcs_round_kernel<NT, DEBUG>, sm, &occ, &cus);
       e != hipSuccess)
@@ -1440,7 +1440,7 @@ static hipError_t launch_chains(const SweepArgs *h, const SweepArgs *d, int K, i
   }
   if (method == kMethodDCS) {
     static LaunchCfg cfg;
-    const int sm = dcs_smem_bytes(make_layout(h[0].n).bytes(), h[0].n);
+    const int sm = dcs_smem_bytes<NT>(make_layout(h[0].n).bytes(), h[0].n);
     int occ = 0, cus = 0;
     if (hipError_t e = launch_config(cfg, (const void *)dcs_chains_kernel<NT>, sm, &occ, &cus); e != hipSuccess)
       return e;
