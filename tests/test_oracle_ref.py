@@ -170,6 +170,29 @@ def test_dcs_treats_censored_as_exact(orc):
     _check_expectations(o, n, Ez, EN, reps, "dcs-cens", S)
 
 
+@pytest.mark.parametrize("n", [3, 5, 10, 15, 20])
+def test_dcs_halley_root_matches_find02(orc, n):
+    """The device spec's DCS jump-time root (hob_halley) against
+    Find02's Brent search (the reference's root finder) on the same draws:
+    every discrete outcome identical, z equal to the CDF evaluation's
+    rounding, and 2.4-3.1x fewer CDF evaluations."""
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 2000, seed=70 + n, censor_frac=0.3)
+    out = {}
+    try:
+        for brent in (True, False):
+            orc.set_dcs_brent(brent)
+            out[brent] = orc.dev_sweep(4, S, s, y, cen, key=(0xD5 + n, 3), sweep=2)
+    finally:
+        orc.set_dcs_brent(False)
+    a, b = out[True], out[False]
+    for f in ("B", "pre", "N", "ndraw", "flags"):
+        assert np.array_equal(a[f], b[f]), f
+    rel = np.abs(a["z"] - b["z"]).max() / np.abs(a["z"]).max()
+    assert rel < 1e-9, rel
+    assert a["stats"][1] > 2.2 * b["stats"][1], (a["stats"][1], b["stats"][1])
+
+
 def test_censored_expectations_by_forward_simulation():
     """The censored analytics above against brute-force forward simulation
     conditioned on Y > y (the survey's censored probe)."""
