@@ -122,6 +122,8 @@ class OracleLib:
                                   _dp, C.c_long, _ip, _dp, _dp, C.c_int]
         L.orc_rgamma_ctr_v.argtypes = [C.c_uint32, C.c_uint32, C.c_double, C.c_double, C.c_long, _dp]
         L.orc_eig.argtypes = [C.c_int, _dp, _dp, _dp, _dp]
+        L.orc_eig_refine.argtypes = [C.c_int, _dp, _dp, _dp, _dp, _dp, _dp]
+        L.orc_eig_fallback_count.restype = C.c_long
         L.orc_set_dcs_brent.argtypes = [C.c_int]
 
     def set_seed(self, seed: int) -> None:
@@ -187,6 +189,17 @@ class OracleLib:
         self.lib.orc_gibbs_z(int(dev), it, mhit, method, n, len(nu), a["nu"], a["zeta"], a["T"], a["C"], a["y"],
                              len(y), a["censored"], a["start"], a["res"], int(zexp))
         return a["res"].reshape(len(nu), it).T.copy()
+
+    def eig_refine(self, S, Q0, Qi0):
+        """The resident chain's warm-start refinement (pht_eig_refine) of the
+        eigensystem (Q0, Qi0) for S: (rc, evals, Q, Qinv), rc 2 = not
+        converged (the chain then runs the full QR)."""
+        S = np.asarray(S, np.float64)
+        n = S.shape[0]
+        f = lambda M: np.ascontiguousarray(np.asarray(M, np.float64).reshape(-1, order="F"))
+        ev, Q, Qi = np.zeros(n), np.zeros(n * n), np.zeros(n * n)
+        rc = self.lib.orc_eig_refine(n, f(S), f(Q0), f(Qi0), ev, Q, Qi)
+        return rc, ev, Q.reshape(n, n, order="F"), Qi.reshape(n, n, order="F")
 
     def set_dcs_brent(self, on: bool) -> None:
         """dev variant's DCS root finder: Find02's Brent search (on) or the

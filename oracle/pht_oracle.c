@@ -113,10 +113,29 @@ int orc_eig(int n, const double *S, double *evals, double *Q, double *Qinv) {
   return pht_eig(n, S, evals, Q, Qinv, &w);
 }
 
+/* diagnostics: warm starts that fell back to the full QR (tests) */
+static long orc_eig_fallbacks = 0;
+long orc_eig_fallback_count(void) { long v = orc_eig_fallbacks; orc_eig_fallbacks = 0; return v; }
+
+/* the resident chain's warm start (pht_eig_refine); Q0/Qi0 the previous
+ * eigensystem (n x n, column-major) */
+int orc_eig_refine(int n, const double *S, const double *Q0, const double *Qi0, double *evals, double *Q, double *Qinv) {
+  static double H[ORC_MAXN * ORC_MAXN], V[ORC_MAXN * ORC_MAXN], X[ORC_MAXN * ORC_MAXN],
+      G[2 * ORC_MAXN * ORC_MAXN], ort[ORC_MAXN], scale[ORC_MAXN], d[ORC_MAXN];
+  pht_eig_ws w = {H, V, X, G, ort, scale, d};
+  return pht_eig_refine(n, S, Q0, Qi0, evals, Q, Qinv, &w);
+}
+
 /* Per-sweep data (src/PHT_MCMC_Aslett.c:279-297, :320-332) + device-mode
  * precomputed products.  method | ORC_DEVEIG: the eigensystem by orc_eig
  * (the device-resident chain) instead of LAPACK. */
 int orc_sp_build(orc_sp *sp, int n, const double *S, const double *s, int method) {
+  static double Q0[ORC_MAXN * ORC_MAXN], Qi0[ORC_MAXN * ORC_MAXN];
+  const int warm = (method & ORC_DEVEIG) && (method & ORC_DEVEIG_WARM);
+  if (warm) {
+    memcpy(Q0, sp->Q, sizeof Q0);
+    memcpy(Qi0, sp->Qinv, sizeof Qi0);
+  }
   memset(sp, 0, sizeof *sp);
   sp->n = n;
   memcpy(sp->S, S, sizeof(double) * n * n);
@@ -137,8 +156,16 @@ int orc_sp_build(orc_sp *sp, int n, const double *S, const double *s, int method
     Pf[i + n * n] = Pf[i + n * n] / rsumfull;
   }
   if (method & (ORC_ECS | ORC_DCS)) {
-    sp->eig_info = (method & ORC_DEVEIG) ? orc_eig(n, S, sp->evals, sp->Q, sp->Qinv)
-                                         : orc_eigen(n, S, sp->evals, sp->Q, sp->Qinv);
+    if (method & ORC_DEVEIG) {
+      int rc = warm ? orc_eig_refine(n, S, Q0, Qi0, sp->evals, sp->Q, sp->Qinv) : PHT_EIG_NOCONV;
+      if (rc != PHT_EIG_OK) {
+        if (warm && n <= PHT_EIG_REFINE_MAXN) orc_eig_fallbacks++;
+        rc = orc_eig(n, S, sp->evals, sp->Q, sp->Qinv);
+      }
+      sp->eig_info = rc;
+    } else {
+      sp->eig_info = orc_eigen(n, S, sp->evals, sp->Q, sp->Qinv);
+    }
     double one[ORC_MAXN];
     for (int i = 0; i < n; i++) one[i] = 1.0;
     orcR_gemv_n(n, sp->Qinv, s, sp->Qinv_s);
@@ -574,7 +601,8 @@ void orc_gibbs_z(int dev, int it, int mhit, int method, int n, int m, const doub
   int disp = dispatch(method);
   for (int iter = 1; iter < it; iter++) {
     if (!disp) continue; /* "CRITICAL ERROR: Unknown sampling method" */
-    orc_sp_build(sp, n, S, s, (disp == ORC_MHRS ? ORC_MHRS : method) | (dev == 2 ? ORC_DEVEIG : 0));
+    orc_sp_build(sp, n, S, s,
+                 (disp == ORC_MHRS ? ORC_MHRS : method) | (dev == 2 ? ORC_DEVEIG | (iter > 1 ? ORC_DEVEIG_WARM : 0) : 0));
     if (!dev) {
       orc_ref_sweep(sp, method, mhit, y, censored, l, z, Bt, Nt, NULL, NULL, NULL, NULL, NULL, NULL, NULL);
     } else {

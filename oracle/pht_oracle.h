@@ -18,6 +18,9 @@
 /* orc_sp_build only: the eigensystem by include/pht_eigen.h (the
  * device-resident chain), not LAPACK */
 #define ORC_DEVEIG 0x100
+/* with ORC_DEVEIG: refine sp's current eigensystem (the previous sweep's)
+ * first, as the resident chain does after its first sweep */
+#define ORC_DEVEIG_WARM 0x200
 
 /* per-sweep data handed to the samplers (src/PHT_MCMC_Aslett.c:276-333).
  * All matrices column-major A[i + j*n]; Pfull is n x (n+1). */

@@ -37,8 +37,9 @@ constexpr int kResMaxM = (kMaxN + 1) * (kMaxN + 1);
 /*
  * ECS/DCS: the spectral part of build_params (gibbs_host.cpp; the
  * reference's src/PHT_MCMC_Aslett.c:320-332) from this sweep's S, s, P in
- * the parameter block: the eigensystem by pht_eig (include/pht_eigen.h) in
- * place of LAPACK, then Q^-1 s and Q^-1 1 in the reference BLAS dgemv order
+ * the parameter block: the eigensystem (include/pht_eigen.h: refined from
+ * the previous sweep's, the full QR at init or when that fails) in place of
+ * LAPACK, then Q^-1 s and Q^-1 1 in the reference BLAS dgemv order
  * and the products QQs, W, QQ1, V, piQ with build_params's fma order.  A
  * failed eigensystem sets err bit 3 and leaves the previous sweep's spectral
  * data in place (finite values; the host reports the error after the run);
@@ -50,8 +51,11 @@ __device__ __forceinline__ void spectral(const ResidentArgs &r, int n, const Lay
   const int tid = threadIdx.x, nt = blockDim.x;
   pht_eig_ws w;
   w.H = eH; w.V = eV; w.X = eX; w.G = eG; w.ort = eort; w.scale = escale; w.d = ed;
-  /* Q^-1 lands in eX (free once the eigenvectors are back-transformed) */
-  const int rc = pht_eig(n, dv + L.S, eev, eQ, eX, &w);
+  /* Q^-1 lands in eX (free once the eigenvectors are back-transformed).
+   * After the first sweep: refined from the previous sweep's eigensystem
+   * (the block still holds it), the full QR only if that does not converge */
+  int rc = r.init ? PHT_EIG_NOCONV : pht_eig_refine(n, dv + L.S, dv + L.Q, dv + L.Qinv, eev, eQ, eX, &w);
+  if (rc != PHT_EIG_OK) rc = pht_eig(n, dv + L.S, eev, eQ, eX, &w);
   __syncthreads();
   if (rc != PHT_EIG_OK) {
     if (tid == 0) atomicOr(r.err, 8);
