@@ -81,11 +81,31 @@ def attach_rccl(sweeper, dist, device: str, n_words: int = 256) -> bool:
 
     from . import RCCL_ID_BYTES, rccl_unique_id
 
-    t = torch.zeros(RCCL_ID_BYTES, dtype=torch.uint8, device=device)
+    # every rank reaches every collective below whatever fails locally, so a
+    # failure on one rank becomes a common "fall back" verdict, not a hang
+    def agree(ok):
+        v = torch.tensor([1 if ok else 0], dtype=torch.int64, device=device)
+        dist.all_reduce(v, op=dist.ReduceOp.MIN)
+        return bool(v.item())
+
+    t = torch.zeros(RCCL_ID_BYTES + 1, dtype=torch.uint8, device=device)  # id + "id made" byte
     if dist.get_rank() == 0:
-        t.copy_(torch.frombuffer(bytearray(rccl_unique_id()), dtype=torch.uint8))
+        try:
+            t[:RCCL_ID_BYTES].copy_(torch.frombuffer(bytearray(rccl_unique_id()), dtype=torch.uint8))
+            t[RCCL_ID_BYTES] = 1
+        except Exception:  # noqa: BLE001 - rank 0 has no RCCL: everyone falls back
+            t[RCCL_ID_BYTES] = 0
     dist.broadcast(t, 0)
-    sweeper.attach_rccl(bytes(t.cpu().numpy().tobytes()), dist.get_world_size(), dist.get_rank())
+    host = t.cpu().numpy()
+    if host[RCCL_ID_BYTES] == 0:
+        return False
+    try:
+        sweeper.attach_rccl(bytes(host[:RCCL_ID_BYTES].tobytes()), dist.get_world_size(), dist.get_rank())
+        attached = True
+    except Exception:  # noqa: BLE001 - reported through the verdict
+        attached = False
+    if not agree(attached):
+        return False
     mine = rccl_selftest_vector(dist.get_rank(), n_words)
     lib_sum = mine.copy()
     ok = 1
@@ -97,9 +117,7 @@ def attach_rccl(sweeper, dist, device: str, n_words: int = 256) -> bool:
     dist.all_reduce(ref)
     if ok and not np.array_equal(lib_sum, ref.cpu().numpy()):
         ok = 0
-    verdict = torch.tensor([ok], dtype=torch.int64, device=device)
-    dist.all_reduce(verdict, op=dist.ReduceOp.MIN)
-    return bool(verdict.item())
+    return agree(ok)
 
 
 def max_over_ranks(dist, values, device: str = "cpu"):

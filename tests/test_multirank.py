@@ -86,3 +86,55 @@ def test_shard_range_partitions():
             assert r[0][0] == 0 and r[-1][1] == N
             assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
             assert max(h - lo for lo, h in r) - min(h - lo for lo, h in r) <= 1
+
+
+class _FakeSweeper:
+    """Stands in for a GPU Sweeper in attach_rccl's failure paths (no GPU
+    here): attach fails on the ranks listed, the library all-reduce is
+    never reached."""
+
+    def __init__(self, fail_attach):
+        self.fail_attach = fail_attach
+
+    def attach_rccl(self, uid, world, rank):
+        if self.fail_attach:
+            raise RuntimeError("ncclCommInitRank failed (fake)")
+
+    def rccl_allreduce(self, buf):
+        raise RuntimeError("not attached (fake)")
+
+
+def _attach_worker(rank, world, port, mode):
+    import sys
+
+    sys.path.insert(0, REPO)
+    import torch.distributed as dist
+
+    import phasetype_amd as P
+    from phasetype_amd import dist as D
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        if mode == "no_id":  # rank 0 cannot make an RCCL id
+            def boom():
+                raise RuntimeError("no RCCL (fake)")
+            P.rccl_unique_id = boom
+            sw = _FakeSweeper(False)
+        else:  # the communicator fails on the last rank only
+            P.rccl_unique_id = lambda: bytes(P.RCCL_ID_BYTES)
+            sw = _FakeSweeper(rank == world - 1)
+        assert D.attach_rccl(sw, dist, "cpu") is False
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["no_id", "attach_fails_on_one_rank"])
+def test_attach_rccl_failures_fall_back_on_every_rank(mode):
+    """bench.py's in-library RCCL reduce: a failure on any rank (no RCCL id
+    on rank 0, a communicator that fails on one rank) must return False on
+    every rank — the callback reduce is then used — instead of leaving the
+    other ranks waiting in a collective."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_attach_worker, args=(2, _free_port(), mode), nprocs=2, join=True)
