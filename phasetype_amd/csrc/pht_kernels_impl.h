@@ -1231,7 +1231,7 @@ static int smem_bytes_unif(int n, int K) {
   return ((smem_bytes(n) + 15) & ~15) + 3 * (K + 1) * 8 + n * n * 12 + n * 4; /* + predecessor lists */
 }
 
-template <int NT, bool DEBUG, bool ALDS>
+template <int NT, bool DEBUG>
 __device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
@@ -1248,8 +1248,8 @@ __device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsi
   PHT_LDS double *tl = (PHT_LDS double *)(lsm + ((pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 15) & ~15));
   const double *T = a.utab;
   const int K = (int)T[2]; /* rows of this sweep's table (<= a.uK, the LDS sizing) */
-  /* invk, ax, ac (and with ALDS the forward vectors A) staged into LDS */
-  const long nstage = 3L * (K + 1) + (ALDS ? (long)(K + 1) * n : 0L);
+  /* invk, ax, ac staged into LDS */
+  const long nstage = 3L * (K + 1);
   for (long k = threadIdx.x; k < nstage; k += blockDim.x) tl[k] = T[4 + k];
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
@@ -1260,13 +1260,11 @@ __device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsi
   PHT_LDS int *pc = (PHT_LDS int *)(pv + n * n), *np = pc + n * n;
   unif_preds<NT>(P, T[1], pv, pc, np);
   __syncthreads();
-  typedef typename std::conditional<ALDS, const PHT_LDS double *, const double *>::type APtr;
-  UnifTab<APtr> U;
+  UnifTab<const double *> U;
   U.invk = tl;
   U.ax = tl + (K + 1);
   U.ac = tl + 2 * (K + 1);
-  if constexpr (ALDS) U.A = tl + 3 * (K + 1);
-  else U.A = T + 4 + 3 * (K + 1);
+  U.A = T + 4 + 3 * (K + 1);
   U.pv = pv;
   U.pc = pc;
   U.np = np;
@@ -1309,9 +1307,9 @@ __device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsi
   flush_stats(a.stats, zq, Bc, Nc, xc, n);
 }
 
-template <int NT, bool DEBUG, bool ALDS>
+template <int NT, bool DEBUG>
 __global__ void __launch_bounds__(kBlock) unif_kernel(SweepArgs a) {
-  unif_body<NT, DEBUG, ALDS>(a, blockIdx.x, gridDim.x);
+  unif_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
 }
 
 template <int NT, bool DEBUG>
@@ -1319,27 +1317,17 @@ static hipError_t launch_unif(const SweepArgs &a, hipStream_t st) {
   if (a.utab == nullptr || a.uK < 1 || a.uK > kUnifMaxK || a.begin != 0) return hipErrorInvalidValue;
   if (hipError_t e = launch_unif_table<NT>(a, st); e != hipSuccess) return e;
   if (a.count < 1) return hipGetLastError();
-  /* PHT_UNIF_ALDS=1: the forward vectors in LDS too (same results; measured
-   * no faster than L2-resident vectors at n = 10..20, r03 — so opt-in) */
-  static LaunchCfg cfg, cfgl;
+  /* the forward vectors stay in the global table (L2): staging them in LDS
+   * as well measured no faster at n = 10..20 (r03) */
+  static LaunchCfg cfg;
   const int sm = smem_bytes_unif(a.n, a.uK);
-  const int sml = sm + (a.uK + 1) * a.n * 8;
-  int occ = 0, cus = 0, occl = 0, cusl = 0;
-  if (hipError_t e = launch_config(cfg, (const void *)unif_kernel<NT, DEBUG, false>, sm, &occ, &cus); e != hipSuccess)
+  int occ = 0, cus = 0;
+  if (hipError_t e = launch_config(cfg, (const void *)unif_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
     return e;
-  static const int force = getenv("PHT_UNIF_ALDS") ? atoi(getenv("PHT_UNIF_ALDS")) : -1;
-  bool alds = false;
-  if (force == 1 && sml <= 160 * 1024) {
-    if (hipError_t e = launch_config(cfgl, (const void *)unif_kernel<NT, DEBUG, true>, sml, &occl, &cusl);
-        e != hipSuccess)
-      return e;
-    alds = true;
-  }
-  long grid = (long)cus * (alds ? occl : occ);
+  long grid = (long)cus * occ;
   const long want = (a.count + kClaimChunk - 1) / kClaimChunk;
   if (grid > want) grid = want;
-  if (alds) hipLaunchKernelGGL((unif_kernel<NT, DEBUG, true>), dim3((unsigned)grid), dim3(kBlock), sml, st, a);
-  else hipLaunchKernelGGL((unif_kernel<NT, DEBUG, false>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
+  hipLaunchKernelGGL((unif_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
   return hipGetLastError();
 }
 
@@ -1380,7 +1368,7 @@ __global__ void __launch_bounds__(kUnifTabThreads) unif_table_chains_kernel(cons
 }
 template <int NT>
 __global__ void __launch_bounds__(kBlock) unif_chains_kernel(const SweepArgs *args, int K, unsigned nblk) {
-  unif_body<NT, false, false>(args[blockIdx.x % (unsigned)K], blockIdx.x / (unsigned)K, nblk);
+  unif_body<NT, false>(args[blockIdx.x % (unsigned)K], blockIdx.x / (unsigned)K, nblk);
 }
 /* MHRS: per chain, the first-success records to "unresolved" and the queue
  * counters to zero (grid-stride over each chain's tasks) */

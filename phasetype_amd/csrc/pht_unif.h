@@ -64,7 +64,7 @@ constexpr double kUnifMaxLam = 1300.0; /* w_0 = 2^-1000 keeps every weight finit
 template <class APtr>
 struct UnifTab {
   const PHT_LDS double *invk, *ax, *ac; /* staged in LDS */
-  APtr A;                               /* row k at A + k n: LDS when it fits (unif_kernel), else global */
+  APtr A;                               /* row k at A + k n (the global table, L2-resident) */
   const PHT_LDS double *pv;             /* predecessors of b in R: values R_{c,b} at pv[b n + q], */
   const PHT_LDS int *pc, *np;           /* c at pc[b n + q], q < np[b] (unif_preds) */
   int K;

@@ -501,20 +501,3 @@ def _oracle_chain_zexp(orc, it, mhit, method, n, nu, zeta, T, Cm, y, cen, zexp):
                           cen, zexp)
 
 
-@pytest.mark.parametrize("alds", ["0", "1"])
-def test_unif_lds_table_invariance(gpu, monkeypatch, alds):
-    """UNIF with the forward vectors staged in LDS or read from L2
-    (PHT_UNIF_ALDS=1|0; read once per process, so exercised only if no
-    earlier UNIF launch cached it) gives the same statistics."""
-    n = 10
-    S, s = bd_exit(n)
-    y, cen = simulate_ph(S, s, 20000, seed=41, censor_frac=0.3)
-    zexp = P.zexp_for(y)
-    sw = P.Sweeper(n, 8)
-    sw.set_obs(y, cen)
-    ref = sw.sweep(S, s, key=(2, 9), sweep=3, zexp=zexp)
-    monkeypatch.setenv("PHT_UNIF_ALDS", alds)
-    got = sw.sweep(S, s, key=(2, 9), sweep=3, zexp=zexp)
-    sw.close()
-    L = 2 * n + n * n
-    assert np.array_equal(ref[:L], got[:L]) and got[L] == len(y)
