@@ -375,6 +375,7 @@ struct pht_ctx {
   double ymax = 0.0;                     /* largest y of the shard (UNIF table length) */
   double *d_utab = nullptr;              /* UNIF per-sweep table (pht_unif.h) */
   long utab_cap = 0;                     /* its capacity in doubles */
+  int *d_dcsb = nullptr;                 /* DCS: per-position end states (dcs_end_kernel) */
   /* debug buffers */
   long long *d_zq = nullptr;
   int *d_N = nullptr, *d_B = nullptr, *d_pre = nullptr, *d_flags = nullptr;
@@ -546,6 +547,7 @@ static int group_sweep(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   a.sweep = sweep;
   a.zscale = ldexp(1.0, zexp);
   a.dcsbrent = dcs_brent();
+  a.dcsb = nullptr; /* the chains launch computes the end states in its round kernel */
   a.stats = ds;
   SweepArgs ae = a, ac = a;
   if (g->method == kMethodECS) {
@@ -607,6 +609,8 @@ static void ctx_free_obs(pht_ctx *c) {
   if (c->d_utab) (void)hipFree(c->d_utab);
   c->d_utab = nullptr;
   c->utab_cap = 0;
+  if (c->d_dcsb) (void)hipFree(c->d_dcsb);
+  c->d_dcsb = nullptr;
   c->d_y = nullptr; c->d_cens = nullptr; c->d_gid = nullptr;
   c->d_mbest = c->d_mq0 = c->d_mq1 = nullptr;
   c->d_mcnt = nullptr;
@@ -805,6 +809,9 @@ extern "C" void pht_ctx_destroy(pht_ctx *c) {
   delete c;
 }
 
+/* DCS end-state pre-pass from this many observations per shard */
+constexpr long kDcsPrepassMin = 100000;
+
 /*
  * Upload this shard's observations.  obs0 = global index of y[0]; the
  * Philox counter of observation i is obs0 + i whatever the shard layout.
@@ -866,6 +873,15 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
     HIPCHK(hipMalloc(&c->d_mq0, sizeof(uint32_t) * tasks));
     HIPCHK(hipMalloc(&c->d_mq1, sizeof(uint32_t) * tasks));
     HIPCHK(hipMalloc(&c->d_mcnt, sizeof(unsigned) * kMhrsCounters));
+  }
+  /* DCS: for large shards the end states come from a pre-pass kernel
+   * (dcs_end_kernel; results identical).  Measured (profiles/r03/dcs_prepass/):
+   * -4 % kernel time at n = 10, N = 10^6, -2 % at cfg5, flat at n = 5/20,
+   * +6 % at N = 200 (one more launch).  PHT_DCS_PREPASS=1|0 forces it. */
+  {
+    const char *e = getenv("PHT_DCS_PREPASS");
+    const bool pre = e ? atoi(e) != 0 : count >= kDcsPrepassMin;
+    if (c->method == kMethodDCS && pre) HIPCHK(hipMalloc(&c->d_dcsb, sizeof(int) * count));
   }
   return 0;
 }
@@ -1007,6 +1023,7 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   a.sweep = sweep;
   a.zscale = ldexp(1.0, zexp);
   a.dcsbrent = dcs_brent();
+  a.dcsb = c->d_dcsb;
   a.stats = c->d_stats;
   a.mbest = c->d_mbest;
   a.mq0 = c->d_mq0;
@@ -1615,6 +1632,7 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
   a.k1 = k1;
   a.zscale = ldexp(1.0, zexp);
   a.dcsbrent = dcs_brent();
+  a.dcsb = c->d_dcsb;
   a.stats = c->d_stats;
   a.mbest = c->d_mbest;
   a.mq0 = c->d_mq0;

@@ -207,6 +207,45 @@ __device__ __forceinline__ double hob_halley(const Par<NT> &P, const DcsE<NT> &E
   return root;
 }
 
+/* A new observation's end state b ~ (pi e^{yS})_b s_b (LJMA_Hobolth_endState,
+ * src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:11-51) from ey_i = e^{lambda_i
+ * y} and the target uniform u: shared by the round kernel and the end-state
+ * pre-pass (dcs_end_kernel), so both give the same b bit for bit.  (The
+ * weights are recomputed in the scan, as dcs() does.) */
+template <int NT, class EV>
+__device__ __forceinline__ int dcs_end_state(const Par<NT> &P, const EV &ey, double u, int &flags) {
+  const int n = P.n();
+  double av[PHT_VEC(NT)];
+#pragma unroll
+  for (int i = 0; i < n; i++) av[i] = P.piQ(i) * ey.get(i);
+  double sum = 0.0;
+#pragma unroll 1
+  for (int k = 0; k < n; k++) {
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; i++) acc = fma(av[i], P.Qinv(i, k), acc);
+    sum += acc * P.s(k);
+  }
+  const double tg = u * sum;
+  double sofar = 0.0;
+  int q = 0;
+#pragma unroll 1
+  for (; q < n; q++) {
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; i++) acc = fma(av[i], P.Qinv(i, q), acc);
+    sofar += acc * P.s(q);
+    if (!(sofar < tg)) break;
+  }
+  if (q == n) {
+    flags |= kFlagScanEnd;
+    q = n - 1;
+  }
+  return q;
+}
+/* the pre-pass's per-position record: b, and the scan-overrun flag */
+constexpr int kDcsEndFlag = 0x100;
+
 /* LDS layout after the sweep kernels' common part (parameter block,
  * accumulators, cursor): near masks [n] u32, then rinv [n*n] f64 */
 __host__ __device__ constexpr int dcs_rinv_offset(int pbytes, int n) {
@@ -227,6 +266,7 @@ struct DcsLane {
   int phase;
   double y, t;
   int j, lastj, b, njump;
+  int endrec; /* the pre-pass's record of this observation (SweepArgs::dcsb) */
 };
 
 /*
@@ -328,35 +368,14 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
    * src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:11-51) from its
    * e^{lambda_i y}, start state, and the jump loop's head */
   auto new_obs = [&](const DcsE<NT> &ey) {
-    /* (the weights are recomputed in the scan, as dcs() does, instead of
-     * held in registers) */
-    double av[PHT_VEC(NT)];
-#pragma unroll
-    for (int i = 0; i < n; i++) av[i] = P.piQ(i) * ey.get(i);
-    double sum = 0.0;
-#pragma unroll 1
-    for (int k = 0; k < n; k++) {
-      double acc = 0.0;
-#pragma unroll
-      for (int i = 0; i < n; i++) acc = fma(av[i], P.Qinv(i, k), acc);
-      sum += acc * P.s(k);
+    if (a.dcsb) { /* computed by dcs_end_kernel from the same word */
+      const int v = st.endrec;
+      (void)pht_next_w(&ln.r);
+      if (v & kDcsEndFlag) ln.flags |= kFlagScanEnd;
+      st.b = v & (kDcsEndFlag - 1);
+    } else {
+      st.b = dcs_end_state(P, ey, dev_u(ln.r), ln.flags);
     }
-    const double tg = dev_u(ln.r) * sum;
-    double sofar = 0.0;
-    int q = 0;
-#pragma unroll 1
-    for (; q < n; q++) {
-      double acc = 0.0;
-#pragma unroll
-      for (int i = 0; i < n; i++) acc = fma(av[i], P.Qinv(i, q), acc);
-      sofar += acc * P.s(q);
-      if (!(sofar < tg)) break;
-    }
-    if (q == n) {
-      ln.flags |= kFlagScanEnd;
-      q = n - 1;
-    }
-    st.b = q;
     const double target = dev_u(ln.r);
     const int B = pistart(P, target, ln.flags);
     sk.start(B);
@@ -395,6 +414,7 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
           sk.dpre = a.dbg_pre + pos;
         }
         st.y = a.y[pos];
+        if (a.dcsb) st.endrec = a.dcsb[pos];
         st.t = 0.0;
         st.phase = kDcsNew;
       }

@@ -46,6 +46,8 @@ struct SweepArgs {
   int nmain;
   int rowprio;                 /* ECS exact: wave priority of the row blocks (s_setprio 0-3) */
   int dcsbrent;                /* DCS: jump times by Find02's Brent search instead of hob_halley (pht_dcs_round.h) */
+  int *dcsb;                   /* DCS: per position the end state (| flag), written by dcs_end_kernel ahead of
+                                  the round kernel; nullptr: computed in the round kernel */
   /* MHRS attempt search (pht_kernels.hip, MHRS section): per chain task
    * (position * (1 + mhit) + c) its first success (attempt << 8 | pre), two
    * task queues and the queue counters; allocated by the host for MHRS */

@@ -1073,8 +1073,44 @@ __attribute__((amdgpu_waves_per_eu(dcs_waves<NT>())))
 dcs_round_kernel(SweepArgs a) {
   dcs_round_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
 }
+/* DCS end-state pre-pass: for every position of the launch, the end state
+ * the round kernel would draw (dcs_end_state on e^{lambda_i y} and the
+ * observation stream's first word), into a.dcsb */
+template <int NT>
+__global__ void __launch_bounds__(kBlock) dcs_end_kernel(SweepArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const Par<NT> P = stage_params<NT>(a, (PHT_LDS unsigned char *)smem);
+  pht_stage_math_tables();
+  __syncthreads();
+  const int n = P.n();
+  for (long p = (long)blockIdx.x * kBlock + threadIdx.x; p < a.count; p += (long)gridDim.x * kBlock) {
+    const long pos = a.begin + p;
+    const double x = a.y[pos] - 0.0; /* the round kernel's y - t at t = 0 */
+    DcsE<NT, false> ey;
+#pragma unroll
+    for (int i = 0; i < n; i++) ey.set(i, pht_exp_neg(P.evals(i) * x));
+    pht_stream r;
+    pht_stream_init(&r, a.k0, a.k1, a.gid[pos], 0u, a.sweep);
+    int flags = 0;
+    const int b = dcs_end_state(P, ey, dev_u(r), flags);
+    a.dcsb[pos] = b | (flags ? kDcsEndFlag : 0);
+  }
+}
+
 template <int NT, bool DEBUG>
 static hipError_t launch_dcs_round(const SweepArgs &a, hipStream_t st) {
+  /* every observation's end state first, one thread per position (the round
+   * kernel would run that n^2 scan in almost every round: some lane of the
+   * wavefront starts an observation) */
+  if (a.dcsb && a.count > 0) {
+    static LaunchCfg cfge;
+    const int sme = make_layout(a.n).bytes();
+    int occe = 0, cuse = 0;
+    if (hipError_t e = launch_config(cfge, (const void *)dcs_end_kernel<NT>, sme, &occe, &cuse); e != hipSuccess)
+      return e;
+    const long ge = std::min<long>((a.count + kBlock - 1) / kBlock, (long)cuse * occe);
+    hipLaunchKernelGGL((dcs_end_kernel<NT>), dim3((unsigned)ge), dim3(kBlock), sme, st, a);
+  }
   static LaunchCfg cfg;
   const int sm = dcs_smem_bytes<NT>(make_layout(a.n).bytes(), a.n); /* + near masks, reciprocals */
   int occ = 0, cus = 0;

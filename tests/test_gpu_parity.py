@@ -96,6 +96,28 @@ def test_dcs_brent_root_bitexact(gpu, orc, monkeypatch, n, N, cf):
     assert P.split_stats(h["stats"], n)[3][5] * 2 < P.split_stats(g["stats"], n)[3][5]
 
 
+@pytest.mark.parametrize("n,N,cf", [(3, 2000, 0.3), (10, 1000, 0.0), (15, 300, 0.3)])
+def test_dcs_end_state_prepass_bitexact(gpu, orc, monkeypatch, n, N, cf):
+    """PHT_DCS_PREPASS=1: the end states from the pre-pass kernel
+    (dcs_end_kernel; by default only from 100k observations per shard) give
+    the same per-observation results as the oracle, bit for bit."""
+    monkeypatch.setenv("PHT_DCS_PREPASS", "1")
+    S0, s0 = bd_exit(n)
+    y, cen = simulate_ph(S0, s0, N, seed=3000 + n, censor_frac=cf)
+    S, s = _perturbed(n, n + 2)
+    key, sweep = (0x999 + n, 0x17), 5
+    zexp = int(orc.lib.orc_zexp(np.ascontiguousarray(y), len(y)))
+    o = orc.dev_sweep(4, S, s, y, cen, key=key, sweep=sweep, zexp=zexp)
+    sw = P.Sweeper(n, 4, 1)
+    sw.set_obs(y, cen)
+    g = sw.sweep_debug(S, s, key=key, sweep=sweep, zexp=zexp)
+    st = sw.sweep(S, s, key=key, sweep=sweep, zexp=zexp)
+    sw.close()
+    for f in ("B", "pre", "flags", "ndraw", "zq", "N"):
+        assert np.array_equal(g[f], o[f]), f
+    assert np.array_equal(st[:2 * n + n * n], g["stats"][:2 * n + n * n])
+
+
 @pytest.mark.parametrize("method", [1, 2, 4])
 def test_shard_invariance(gpu, method):
     """Two shards (obs0 offsets) sum to the single-shard block exactly."""
