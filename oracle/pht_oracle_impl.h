@@ -640,7 +640,9 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
       double E0[ORC_MAXN];
       for (int i = 0; i < n; i++) E0[i] = ORC_EXP_NEG(sp->evals[i] * y_t);
       const double den = pht_dot16(sp->QQs + j, n, E0, n);
-      pab = ORC_EXP(fma(sp->S[j + j * n], y_t, sp->logs[j]) - ORC_LOG(den));
+      /* device spec (pht_device.h ecs_absorbs): U den < exp(S_jj y_t + log s_j) */
+      const int absorbs = (den > 0.0) ? (U * den < ORC_EXP(fma(sp->S[j + j * n], y_t, sp->logs[j]))) : (den == 0.0);
+      pab = absorbs ? 2.0 : 0.0; /* U < pab <=> absorbs (U < 1) */
 #else
       /* LJMA_probAbsorb (:120-136) */
       double num = (sp->S[j + j * n] * (y_t)) + log(sp->s[j]);

@@ -648,6 +648,14 @@ __device__ __forceinline__ void ecs_begin(const Par<NT> &P, double y, Lane &ln, 
   st.haveDen = false;
 }
 
+/* LJMA_probAbsorb's test U < exp(S_jj y_t + log s_j - log den) (:120-136,
+ * :251-255) in the device spec's form U den < exp(S_jj y_t + log s_j): the
+ * same decision up to rounding, one logarithm less per test (den = 0
+ * absorbs, den < 0 does not, as the log form) */
+__device__ __forceinline__ bool ecs_absorbs(double U, double Sjj, double y_t, double logs, double den) {
+  return (den > 0.0) ? (U * den < pht_exp(fma(Sjj, y_t, logs))) : (den == 0.0);
+}
+
 /* absorb test at the current state (LJMA_probAbsorb + runif, :251-255);
  * true = the path is complete and its last sojourn has been recorded */
 template <int NT, class Sink>
@@ -668,8 +676,7 @@ __device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink 
       st.haveDen = false;
     }
     const double den = st.haveDen ? st.den : dev_dot16([&](int i) { return P.QQs(j, i); }, st.E0, n);
-    const double pab = pht_exp(fma(P.S(j, j), y_t, P.logs(j)) - pht_log(den));
-    fin = (U < pab);
+    fin = ecs_absorbs(U, P.S(j, j), y_t, P.logs(j), den);
   }
   if (fin) {
     sk.N(j, j);

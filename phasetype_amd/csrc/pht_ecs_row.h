@@ -487,8 +487,7 @@ __device__ __forceinline__ bool row_try_absorb(const Par<NT> &P, const RowId<NT>
     }
     const double den =
         st.haveDen ? st.den : rv_dot(id, rv_coef(id, [&](int i) { return P.QQs(j, i); }), st.E0);
-    const double pab = pht_exp(fma(P.S(j, j), y_t, P.logs(j)) - pht_log(den));
-    fin = (U < pab);
+    fin = ecs_absorbs(U, P.S(j, j), y_t, P.logs(j), den);
   }
   if (fin && id.lead) {
     sk.N(j, j);
@@ -626,7 +625,7 @@ __device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId<NT> &id,
     const bool draw = test && !capj && P.s(j) > 0.0;
     double U = 1.0;
     if (draw) U = dev_u(ln.r);
-    const double pab = pht_exp(fma(P.S(j, j), y_t, P.logs(j)) - pht_log(st.den));
+    const bool absorbs = ecs_absorbs(U, P.S(j, j), y_t, P.logs(j), st.den);
     double xinit[4];
     xinit[0] = (y_t) / 1e6;
     xinit[1] = (y_t) / 3.0;
@@ -641,7 +640,7 @@ __device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId<NT> &id,
     const double xk = (k == 0) ? xinit[0] : (k == 1) ? xinit[1] : (k == 2) ? xinit[2] : xinit[3];
     const double ak = (k == 0) ? acc[0] : (k == 1) ? acc[1] : (k == 2) ? acc[2] : acc[3];
     const double yk = pht_log(ak) + f.Sjj * xk;
-    if (capj || (draw && U < pab)) { /* the path is complete */
+    if (capj || (draw && absorbs)) { /* the path is complete */
       if (capj) ln.flags |= kFlagJumpCap;
       if (id.lead) {
         sk.N(j, j);

@@ -1,6 +1,14 @@
 #!/usr/bin/env python3
-"""Interleaved A/B timing of libPhaseType.so variants in ONE process
-(cdna_hip_programming.md §5.4 rule 24).
+"""Interleaved A/B timing of libPhaseType.so variants, one persistent worker
+process per variant (cdna_hip_programming.md §5.4 rule 24: interleaved
+rounds on one box).
+
+Why not one process: a second library's context in the same process gets
+its two streams mapped onto hardware queues that serialise them, so the ECS
+censored range no longer overlaps the exact range (r03: n = 15, 30 %
+censored, 1.46 ms alone vs 2.44 ms as the second library; profiles/r03/
+ab_isolation/).  Each worker owns one library; the parent sends "run" in
+interleaved order and only one worker uses the GPU at a time.
 
 usage (GPU box): python3 tools/ab.py --libs a.so b.so ... [--rounds 5 --sweeps 10]
 Each variant runs the bench workload (BD-exit(n), N obs, ECS) as a Gibbs
@@ -56,6 +64,15 @@ class Lib:
         return dt, kms.value, res
 
 
+def _worker(conn, path, n, method, y, cen):
+    lb = Lib(path, n, method, y, cen)
+    while True:
+        msg = conn.recv()
+        if msg is None:
+            break
+        conn.send(lb.run(*msg))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--libs", nargs="+", required=True)
@@ -75,15 +92,28 @@ def main():
     zexp = P.zexp_for(y)
     Tf = np.ascontiguousarray(T.reshape(-1, order="F"), np.int32)
     Cm = np.ones(T.size)
-    libs = [Lib(p, n, method, y, cen) for p in a.libs]
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    libs, procs = [], []
+    for p in a.libs:
+        pc, cc = ctx.Pipe()
+        pr = ctx.Process(target=_worker, args=(cc, p, n, method, y, cen), daemon=True)
+        pr.start()
+        libs.append(pc)
+        procs.append(pr)
+
+    def run(conn, *args):
+        conn.send(args)
+        return conn.recv()
+
     for lb in libs:  # warm-up
-        lb.run(3, method, nu, zeta, Tf, Cm, zexp, 1)
+        run(lb, 3, method, nu, zeta, Tf, Cm, zexp, 1)
     times = {p: [] for p in a.libs}
     kern = {p: [] for p in a.libs}
     ref = None
     for r in range(a.rounds):
         for p, lb in zip(a.libs, libs):
-            dt, kms, res = lb.run(a.sweeps + 1, method, nu, zeta, Tf, Cm, zexp, 100 + r)
+            dt, kms, res = run(lb, a.sweeps + 1, method, nu, zeta, Tf, Cm, zexp, 100 + r)
             if r == 0:
                 if ref is None:
                     ref = res
@@ -94,6 +124,9 @@ def main():
     out = {os.path.basename(p): {"ms_per_sweep_median": float(np.median(times[p])), "ms_min": float(np.min(times[p])),
                                  "kernel_ms_median": float(np.median(kern[p]))} for p in a.libs}
     print(json.dumps(out, indent=1))
+    for lb, pr in zip(libs, procs):
+        lb.send(None)
+        pr.join(60)
 
 
 if __name__ == "__main__":
