@@ -21,7 +21,19 @@
 #include "pht_device.h"
 #include "pht_env.h"
 
+#include <type_traits>
+
 namespace pht {
+
+/* the ARMS envelope's x and y in LDS (lane-interleaved, as the exact
+ * kernel's; cum and points beyond PHT_SLOW_K private) at n = 10 only.  The
+ * fully private envelope moves ~2.9 KB of scratch per censored observation
+ * (cfg5: 435 MB per sweep).  One process per library, 30 % censored
+ * (profiles/r03/cens_env_ab2/): n = 10 at 1e6 2.05 -> 1.64 ms; n = 15 (cfg5)
+ * 1.49 -> 1.87 ms (the ~61 KB per block crowds out the concurrent
+ * exact-range kernel); n = 5, 20 unchanged. */
+template <int NT>
+constexpr bool cens_env_lds() { return NT == 10; }
 
 template <int NT, bool DEBUG>
 __device__ __forceinline__ void cens_round_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
@@ -40,6 +52,7 @@ __device__ __forceinline__ void cens_round_body(const SweepArgs &a, unsigned blk
   PHT_LDS unsigned *Bc = (PHT_LDS unsigned *)(xc + kStatExtra);
   PHT_LDS unsigned *Nc = Bc + n;
   PHT_LDS int *cursor = (PHT_LDS int *)(Nc + n * n);
+  PHT_LDS double *envl = (PHT_LDS double *)(lsm + ((pbytes + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 15) & ~15));
   pht_stage_math_tables();
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
@@ -54,7 +67,10 @@ __device__ __forceinline__ void cens_round_body(const SweepArgs &a, unsigned blk
   Lane ln;
   ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
   CensLane cl;
-  EnvPrivate env;
+  typename std::conditional<cens_env_lds<NT>(), EnvLdsXY<PHT_SLOW_K, kBlock>, EnvPrivate>::type env;
+  double spill[2 * EnvLdsXY<PHT_SLOW_K, kBlock>::kSpill];
+  double cumv[100];
+  if constexpr (cens_env_lds<NT>()) env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill, (PHT_PRIV double *)cumv);
   bool have = false, done = false;
   long pos = 0;
   unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
