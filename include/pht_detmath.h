@@ -123,17 +123,32 @@ __shared__ double pht_lds_log_tab[768];
 #define PHT_LOG_TAB pht_log_tab
 #endif
 
-/* Core of every exp below: e^x for |x| <= 709.78 with no special-case
- * handling (callers guarantee the domain or select around it). */
+#ifndef PHT_EXP_LOWK
+#define PHT_EXP_LOWK 1
+#endif
+
+/* Core of every exp below: e^x for -1100 <= x <= 709.78 with no
+ * special-case handling (callers clamp to that domain or select around it).
+ * Below PHT_EXP_LO (-745.13) the result is 0 from the final ldexp's
+ * rounding (checked for the 2e7 doubles below PHT_EXP_LO and on a 1e-4 grid
+ * down to -1100), so the callers clamp there instead of selecting 0. */
 PHT_HD double pht_exp_core(double x) {
   const double INV_LN2_N = 0x1.71547652b82fep+6; /* 64/ln2 */
   const double LN2_HI_N = 0x1.62e42fefa39efp-7;  /* ln2/64 rounded */
   const double LN2_LO_N = 0x1.abc9e3b39803fp-62; /* ln2/64 - LN2_HI_N */
   const double SHIFT = 6755399441055744.0;       /* 1.5 * 2^52 */
-  const double kd = fma(x, INV_LN2_N, SHIFT) - SHIFT; /* round-to-nearest-even integer */
+  const double ts = fma(x, INV_LN2_N, SHIFT); /* SHIFT + round-to-nearest-even integer */
+  const double kd = ts - SHIFT;
   double r = fma(-kd, LN2_HI_N, x);
   r = fma(-kd, LN2_LO_N, r); /* |r| <= ln2/128 */
+#if PHT_EXP_LOWK
+  /* the integer is the low word of ts (its mantissa is 2^51 + ki) */
+  uint64_t tsb;
+  memcpy(&tsb, &ts, sizeof tsb);
+  const int ki = (int)(uint32_t)tsb;
+#else
   const int ki = (int)kd;
+#endif
   const int idx = ki & 63;
   const int k = ki >> 6; /* floor(ki / 64) */
   const double sc = PHT_EXP_TAB[2 * idx], tail = PHT_EXP_TAB[2 * idx + 1];
@@ -149,12 +164,13 @@ PHT_HD double pht_exp_core(double x) {
 
 #define PHT_EXP_HI 709.782712893383973096
 #define PHT_EXP_LO (-745.133219101941108420)
+#define PHT_EXP_FLUSH (-1100.0) /* pht_exp_core(x) = 0 for x <= PHT_EXP_LO's predecessor */
 
 /* e^x for every x: straight-line (selects, no branches on the GPU). */
 PHT_HD double pht_exp(double x) {
-  const double xc = fmin(fmax(x, PHT_EXP_LO), PHT_EXP_HI); /* NaN -> LO */
+  const double xc = fmin(fmax(x, PHT_EXP_FLUSH), PHT_EXP_HI); /* NaN -> FLUSH */
   const double res = pht_exp_core(xc);
-  const double out = (x > PHT_EXP_HI) ? INFINITY : ((x < PHT_EXP_LO) ? 0.0 : res);
+  const double out = (x > PHT_EXP_HI) ? INFINITY : res;
   return (x != x) ? x : out;
 }
 
@@ -165,10 +181,7 @@ PHT_HD double pht_exp_hi(double x) {
 }
 
 /* e^x for x <= 709.78 (no overflow or NaN handling): pht_exp(x) there. */
-PHT_HD double pht_exp_neg(double x) {
-  const double res = pht_exp_core(fmax(x, PHT_EXP_LO));
-  return (x < PHT_EXP_LO) ? 0.0 : res;
-}
+PHT_HD double pht_exp_neg(double x) { return pht_exp_core(fmax(x, PHT_EXP_FLUSH)); }
 
 /* log table, index i + 128 h (i = top 7 mantissa bits of m in [1,2), h = 1
  * when m >= sqrt2 and z = m/2 is used): (invc, logc_hi, logc_lo) with

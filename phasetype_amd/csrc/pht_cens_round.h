@@ -25,15 +25,28 @@
 
 namespace pht {
 
-/* the ARMS envelope's x and y in LDS (lane-interleaved, as the exact
- * kernel's; cum and points beyond PHT_SLOW_K private) at n = 10 only.  The
+/* the ARMS envelope's x and y of the first K points in LDS (lane-
+ * interleaved, as the exact kernel's; cum and later points private).  The
  * fully private envelope moves ~2.9 KB of scratch per censored observation
  * (cfg5: 435 MB per sweep).  One process per library, 30 % censored
- * (profiles/r03/cens_env_ab2/): n = 10 at 1e6 2.05 -> 1.64 ms; n = 15 (cfg5)
- * 1.49 -> 1.87 ms (the ~61 KB per block crowds out the concurrent
- * exact-range kernel); n = 5, 20 unchanged. */
+ * (profiles/r03/cens_env_ab2/): n = 10 at 1e6, K = 15: 1.97 -> 1.68 ms;
+ * n = 20 at 5e5, K = 9: 2.35 -> 2.30 ms (262 -> 223 VGPRs, two waves);
+ * n = 15 (cfg5) K = 15: 1.49 -> 1.87 ms (the ~61 KB per block crowds out
+ * the concurrent exact-range kernel), K = 5 or 9: no gain, so private;
+ * n = 5: unchanged. */
+#ifndef PHT_CENS_K15
+#define PHT_CENS_K15 0
+#endif
+#ifndef PHT_CENS_K20
+#define PHT_CENS_K20 9
+#endif
+/* LDS points per lane (0: the private envelope) */
 template <int NT>
-constexpr bool cens_env_lds() { return NT == 10; }
+constexpr int cens_env_k() { return NT == 10 ? PHT_SLOW_K : NT == 15 ? PHT_CENS_K15 : NT == 20 ? PHT_CENS_K20 : 0; }
+template <int NT>
+constexpr bool cens_env_lds() { return cens_env_k<NT>() > 0; }
+template <int NT>
+constexpr int cens_env_bytes() { return cens_env_lds<NT>() ? 2 * cens_env_k<NT>() * 8 * kBlock : 0; }
 
 template <int NT, bool DEBUG>
 __device__ __forceinline__ void cens_round_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
@@ -67,8 +80,9 @@ __device__ __forceinline__ void cens_round_body(const SweepArgs &a, unsigned blk
   Lane ln;
   ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
   CensLane cl;
-  typename std::conditional<cens_env_lds<NT>(), EnvLdsXY<PHT_SLOW_K, kBlock>, EnvPrivate>::type env;
-  double spill[2 * EnvLdsXY<PHT_SLOW_K, kBlock>::kSpill];
+  using EnvL = EnvLdsXY<(cens_env_lds<NT>() ? cens_env_k<NT>() : 1), kBlock>;
+  typename std::conditional<cens_env_lds<NT>(), EnvL, EnvPrivate>::type env;
+  double spill[2 * EnvL::kSpill];
   double cumv[100];
   if constexpr (cens_env_lds<NT>()) env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill, (PHT_PRIV double *)cumv);
   bool have = false, done = false;

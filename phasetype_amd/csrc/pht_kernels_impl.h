@@ -1134,7 +1134,7 @@ cens_round_kernel(SweepArgs a) {
 template <int NT, bool DEBUG>
 static hipError_t launch_cens_round(const SweepArgs &a, hipStream_t st) {
   static LaunchCfg cfg;
-  const int sm = cens_env_lds<NT>() ? smem_bytes_ecs(a.n) : smem_bytes(a.n);
+  const int sm = ((smem_bytes(a.n) + 4 + 15) & ~15) + cens_env_bytes<NT>();
   int occ = 0, cus = 0;
   if (hipError_t e = launch_config(cfg, (const void *)cens_round_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
     return e;
@@ -1454,7 +1454,7 @@ static hipError_t launch_chains(const SweepArgs *h, const SweepArgs *d, int K, i
   };
   if (method == kMethodECS) {
     static LaunchCfg cfg;
-    const int sm = cens_env_lds<NT>() ? smem_bytes_ecs(h[0].n) : smem_bytes(h[0].n);
+    const int sm = ((smem_bytes(h[0].n) + 4 + 15) & ~15) + cens_env_bytes<NT>();
     int occ = 0, cus = 0;
     if (hipError_t e = launch_config(cfg, (const void *)cens_chains_kernel<NT>, sm, &occ, &cus); e != hipSuccess)
       return e;
