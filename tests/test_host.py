@@ -309,6 +309,23 @@ def test_detmath_exp_accuracy(orc):
     assert out[5] == 1.0 and out[6] == 1.0 and 0 < out[7] < 1e-300  # subnormal result
 
 
+def test_detmath_exp_flush_below_lo(orc):
+    """exp clamps at -1100 and relies on the final ldexp rounding to 0 below
+    PHT_EXP_LO = -745.133... (include/pht_detmath.h): every argument between
+    -1100 and LO's predecessor gives exactly 0, LO itself the least subnormal."""
+    lo = -745.133219101941108420
+    below = np.nextafter(lo, -np.inf)
+    rng = np.random.default_rng(7)
+    x = np.concatenate([rng.uniform(-1100.0, below, 200000),
+                        below - np.arange(20000) * np.spacing(745.0), [-1100.0, -1e300, below]])
+    y = np.ones_like(x)
+    orc.lib.orc_detexp_v(x.ctypes.data_as(C.c_void_p), y.ctypes.data_as(C.c_void_p), C.c_long(len(x)))
+    assert np.all(y == 0.0)
+    one = np.array([lo])
+    orc.lib.orc_detexp_v(one.ctypes.data_as(C.c_void_p), one.ctypes.data_as(C.c_void_p), C.c_long(1))
+    assert one[0] == 5e-324
+
+
 def test_detmath_log_accuracy(orc):
     rng = np.random.default_rng(6)
     x = np.concatenate([np.exp(rng.uniform(-700, 700, 400000)), rng.uniform(0.5, 2.0, 200000),
