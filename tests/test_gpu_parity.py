@@ -21,6 +21,8 @@ CASES = [
     (5, 2000, 0.3, 2, 1), (5, 1000, 0.3, 1, 2), (5, 1500, 0.3, 4, 1),
     (10, 2000, 0.3, 2, 1), (10, 1000, 0.3, 1, 1), (10, 1000, 0.0, 4, 1),
     (15, 600, 0.3, 2, 1), (15, 300, 0.3, 1, 1), (15, 300, 0.3, 4, 1),
+    # n = 20 censored ECS: the censored kernel's 9-point LDS envelope and its private continuation
+    (20, 600, 0.5, 2, 1),
 ]
 
 
