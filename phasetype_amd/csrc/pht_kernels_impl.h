@@ -641,6 +641,7 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
   unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
 #ifdef PHT_ECS_DIAG
   unsigned c_big = 0, c_wbig = 0, c_wround = 0, c_act = 0;
+  unsigned c_start = 0, c_pend = 0, c_new = 0, c_wnew = 0, c_wpend = 0;
 #endif
   for (;;) {
     bool need = false;
@@ -722,9 +723,15 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
       const bool bigl = pend && env.cnt + 2 > kRoundCap;
       c_big += bigl ? 1u : 0u;
       c_act += (need || pend) ? 1u : 0u;
+      c_start += need ? 1u : 0u;
+      c_pend += pend ? 1u : 0u;
+      c_new += (nnew > 0) ? 1u : 0u;
+      const bool wnew = __any(nnew > 0), wpend = __any(pend);
       if ((threadIdx.x & 63) == 0) {
         c_wbig += __any(bigl) ? 1u : 0u;
         c_wround++;
+        c_wnew += wnew ? 1u : 0u;
+        c_wpend += wpend ? 1u : 0u;
       }
     }
 #endif
@@ -751,6 +758,11 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
   lds_add(&xc[7], (unsigned long long)c_wbig);
   lds_add(&xc[8], (unsigned long long)c_wround);
   lds_add(&xc[9], (unsigned long long)c_act);
+  lds_add(&xc[10], (unsigned long long)c_start);
+  lds_add(&xc[11], (unsigned long long)c_pend);
+  lds_add(&xc[12], (unsigned long long)c_new);
+  lds_add(&xc[13], (unsigned long long)c_wnew);
+  lds_add(&xc[14], (unsigned long long)c_wpend);
 #endif
   __syncthreads();
   flush_stats(a.stats, zq, Bc, Nc, xc, n);
