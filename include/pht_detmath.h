@@ -510,6 +510,14 @@ PHT_HD int pht_ecs_init_ok(double lammax, double a, double x3) {
   return lammax * (a > x3 ? a : x3) <= 0x1p-8;
 }
 
+/* E0 = e^{lambda_i y_t} at an observation's FIRST sojourn (device spec, r03):
+ * (F F) F from the point-2b vector F of that sojourn's starting points when
+ * pht_ecs_init_ok holds (the GPU computes F there anyway, so the first absorb
+ * test needs no exponential of its own), else e^{lambda_i y_t} directly.
+ * Later sojourns carry E0 from the previous jump's evaluation, as before.
+ * Error: ~3 ulp plus |lambda y_t| 2^-52 from y_t ~ 3 (y_t - 2b). */
+PHT_HD double pht_ecs_e0_cube(double F) { return (F * F) * F; }
+
 /* Spectral dot product sum_i c_i e_i of the ECS path, in the order every
  * implementation (one lane per observation, or G lanes sharing one) can
  * reproduce: 16 residue slots p_r = c_r e_r (fma with c_{r+16} e_{r+16}

@@ -556,6 +556,9 @@ typedef struct {
   int j;
   double y_t;
   const double *p; /* ref: rate row p_j (p_jj = 0) */
+#if ORC_DEV
+  const double *E0; /* dev: e^{lambda_i y_t} as the GPU carries it (density at d = 0, init4's point a) */
+#endif
 } ORC_FN(ecs_ctx);
 
 #if ORC_DEV
@@ -568,9 +571,10 @@ static double ORC_FN(ecs_dens)(double d, void *vctx) {
   const orc_sp *sp = c->sp;
   const int n = sp->n, j = c->j;
 #if ORC_DEV
-  /* log(sum_i W[j,i] e^{lambda_i (y_t - d)}) + S_jj d */
+  /* log(sum_i W[j,i] e^{lambda_i (y_t - d)}) + S_jj d; at d = 0 the GPU
+   * reuses E0 (pht_device.h EcsDens) */
   double x = c->y_t - d, E[ORC_MAXN];
-  for (int i = 0; i < n; i++) E[i] = ORC_EXP_NEG(sp->evals[i] * x);
+  for (int i = 0; i < n; i++) E[i] = (d == 0.0) ? c->E0[i] : ORC_EXP_NEG(sp->evals[i] * x);
   const double acc = pht_dot16(sp->W + j, n, E, n);
   return ORC_LOG(acc) + sp->S[j + j * n] * d;
 #else
@@ -598,7 +602,7 @@ static void ORC_FN(ecs_init4)(const double xinit[4], double yv[4], void *vctx) {
       const double F = ORC_EXP_NEG(sp->evals[i] * (y_t - xinit[2]));
       E[2][i] = F;
       E[1][i] = F * F;
-      E[0][i] = ORC_EXP_NEG(sp->evals[i] * y_t) * pht_exp_taylor(-sp->evals[i] * xinit[0]);
+      E[0][i] = c->E0[i] * pht_exp_taylor(-sp->evals[i] * xinit[0]);
       E[3][i] = pht_exp_taylor(sp->evals[i] * x3);
     }
   } else {
@@ -624,8 +628,21 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
 #if ORC_DEV
   /* device spec: the remaining time is carried as y_t <- y_t - d (the
    * reference recomputes y - t); the exponentials of moveMass are then
-   * exactly those of the next absorb test, which the GPU reuses */
+   * exactly those of the next absorb test, which the GPU reuses.  E0 =
+   * e^{lambda_i y_t} is carried the same way: at the first sojourn it is
+   * pht_ecs_e0_cube of the starting points' vector F (or direct, outside
+   * pht_ecs_init_ok), after a jump by d the direct e^{lambda_i (y_t - d)},
+   * unchanged after d = 0 */
   double yt = y;
+  double E0[ORC_MAXN];
+  {
+    double lammax = 0.0;
+    for (int i = 0; i < n; i++) lammax = fmax(lammax, fabs(sp->evals[i]));
+    const double a = (y) / 1e6, b2 = ((y) / 3.0) * 2.0;
+    const int ok = pht_ecs_init_ok(lammax, a, y - (y - a));
+    for (int i = 0; i < n; i++)
+      E0[i] = ok ? pht_ecs_e0_cube(ORC_EXP_NEG(sp->evals[i] * (y - b2))) : ORC_EXP_NEG(sp->evals[i] * y);
+  }
 #endif
   for (int njump = 0;; njump++) {
 #if ORC_DEV
@@ -637,8 +654,6 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
     if (sp->s[j] > 0.0) {
       double U = ORC_FN(u)(rng), pab;
 #if ORC_DEV
-      double E0[ORC_MAXN];
-      for (int i = 0; i < n; i++) E0[i] = ORC_EXP_NEG(sp->evals[i] * y_t);
       const double den = pht_dot16(sp->QQs + j, n, E0, n);
       /* device spec (pht_device.h ecs_absorbs): U den < exp(S_jj y_t + log s_j) */
       const int absorbs = (den > 0.0) ? (U * den < ORC_EXP(fma(sp->S[j + j * n], y_t, sp->logs[j]))) : (den == 0.0);
@@ -655,7 +670,11 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
     lastj = j;
     for (int i = 0; i < n; i++) p[i] = sp->S[j + i * n] / (-sp->S[j + j * n]);
     p[j] = 0.0;
+#if ORC_DEV
+    ORC_FN(ecs_ctx) ctx = {sp, j, y_t, p, E0};
+#else
     ORC_FN(ecs_ctx) ctx = {sp, j, y_t, p};
+#endif
     double xinit[4];
     xinit[0] = (y_t) / 1e6;
     xinit[1] = (y_t) / 3.0;
@@ -678,7 +697,8 @@ static void ORC_FN(obs_ecs_exact)(const orc_sp *sp, double y, ORC_FN(rng) *rng, 
     double E[ORC_MAXN], w[ORC_MAXN], sum = 0.0;
     const int *L = sp->succP + j * ORC_MAXN;
     const int cnt = sp->nsuccP[j];
-    for (int i = 0; i < n; i++) E[i] = ORC_EXP_NEG(sp->evals[i] * x);
+    for (int i = 0; i < n; i++) E[i] = (d == 0.0) ? E0[i] : ORC_EXP_NEG(sp->evals[i] * x);
+    for (int i = 0; i < n; i++) E0[i] = E[i];
     for (int q = 0; q < cnt; q++) {
       const int k = L[q];
       const double acc = pht_dot16(sp->QQs + k, n, E, n);

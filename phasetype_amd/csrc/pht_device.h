@@ -581,7 +581,10 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
   /* the four ARMS starting points at once (device spec: pht_ecs_init_ok in
    * include/pht_detmath.h; oracle orcD_ecs_init4) */
   static constexpr bool kInit4 = true;
-  __device__ __forceinline__ void init4(const double xinit[4], double yv[4]) {
+  /* mk: the observation's first sojourn, E0w (= E0) is produced here
+   * (ecs_first_E0's rule, sharing F) */
+  __device__ __forceinline__ void init4(const double xinit[4], double yv[4], bool mk = false,
+                                        double *E0w = nullptr) {
     const int n = P.n();
     auto Wj = [&](int i) { return w(i); };
     const double x3 = y_t - xinit[3];
@@ -591,8 +594,12 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
 #pragma unroll
       for (int i = 0; i < n; i++) F[i] = pht_exp_neg(P.evals(i) * (y_t - xinit[2]));
       acc[2] = dev_dot16(Wj, F, n);
+      /* (E0 in the same loop: F dies here, no extra vector live) */
 #pragma unroll
-      for (int i = 0; i < n; i++) T[i] = F[i] * F[i];
+      for (int i = 0; i < n; i++) {
+        T[i] = F[i] * F[i];
+        if (E0w) E0w[i] = mk ? T[i] * F[i] : E0w[i];
+      }
       acc[1] = dev_dot16(Wj, T, n);
 #pragma unroll
       for (int i = 0; i < n; i++) T[i] = E0[i] * pht_exp_taylor(-P.evals(i) * xinit[0]);
@@ -601,6 +608,10 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
       for (int i = 0; i < n; i++) Elast[i] = pht_exp_taylor(P.evals(i) * x3);
       acc[3] = dev_dot16(Wj, Elast, n);
     } else {
+      if (E0w && mk) {
+#pragma unroll
+        for (int i = 0; i < n; i++) E0w[i] = pht_exp_neg(P.evals(i) * y_t);
+      }
 #pragma unroll
       for (int k = 0; k < 4; k++) {
 #pragma unroll
@@ -624,6 +635,8 @@ struct EcsLane {
   bool haveE0;               /* E0 valid for the current remaining time */
   bool haveDen;              /* den valid for (j, E0) */
   double den;                /* pht_dot16(QQs[j,.], E0): moveMass computed it for the chosen state */
+  bool fold;                 /* the observation's first absorb test is due inside the next round
+                              * (persistent kernel: it shares that round's initial-envelope vector) */
   double E0[PHT_VEC(NT)];    /* e^{λ_i yt}: absorb test / previous moveMass */
 };
 
@@ -636,6 +649,22 @@ __device__ __forceinline__ double lam_max(const Par<NT> &P) {
   return m;
 }
 
+/* E0 = e^{λ_i y_t} at an observation's first sojourn (device spec,
+ * pht_ecs_e0_cube): (F F) F from the vector F = e^{λ_i (y_t - 2b)} of that
+ * sojourn's ARMS starting points when pht_ecs_init_ok holds, else directly */
+template <int NT>
+__device__ __forceinline__ void ecs_first_E0(const Par<NT> &P, double y_t, double lammax, double *E0) {
+  const int n = P.n();
+  const double a = (y_t) / 1e6, b2 = ((y_t) / 3.0) * 2.0;
+  if (pht_ecs_init_ok(lammax, a, y_t - (y_t - a))) {
+#pragma unroll
+    for (int i = 0; i < n; i++) E0[i] = pht_ecs_e0_cube(pht_exp_neg(P.evals(i) * (y_t - b2)));
+  } else {
+#pragma unroll
+    for (int i = 0; i < n; i++) E0[i] = pht_exp_neg(P.evals(i) * y_t);
+  }
+}
+
 template <int NT, class Sink>
 __device__ __forceinline__ void ecs_begin(const Par<NT> &P, double y, Lane &ln, Sink &sk, EcsLane<NT> &st) {
   const double target = dev_u(ln.r);
@@ -646,6 +675,7 @@ __device__ __forceinline__ void ecs_begin(const Par<NT> &P, double y, Lane &ln, 
   st.njump = 0;
   st.haveE0 = false;
   st.haveDen = false;
+  st.fold = false;
 }
 
 /* LJMA_probAbsorb's test U < exp(S_jj y_t + log s_j - log den) (:120-136,
@@ -669,9 +699,8 @@ __device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink 
   } else if (P.s(j) > 0.0) {
     const double y_t = st.yt;
     const double U = dev_u(ln.r);
-    if (!st.haveE0) {
-#pragma unroll
-      for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
+    if (!st.haveE0) { /* the observation's first sojourn */
+      ecs_first_E0(P, y_t, lam_max(P), st.E0);
       st.haveE0 = true;
       st.haveDen = false;
     }
@@ -773,9 +802,8 @@ template <int NT, class Env, class Sink>
 __device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st) {
   const int n = P.n();
   const double y_t = st.yt;
-  if (!st.haveE0) { /* s_j = 0: no absorb test ran at this state */
-#pragma unroll
-    for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
+  if (!st.haveE0) { /* s_j = 0 at the first sojourn: no absorb test ran */
+    ecs_first_E0(P, y_t, lam_max(P), st.E0);
     st.haveE0 = true;
   }
   EcsDens<NT> f = ecs_dens(P, st);

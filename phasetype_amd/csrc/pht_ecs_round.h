@@ -272,23 +272,23 @@ __device__ __forceinline__ double round_metropolis(const Env &e, const WPt &p, d
  */
 template <int NT, class Env, class Sink>
 __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st, bool start,
-                                          bool &pend, ArmsPend &pd, double lam) {
+                                          bool &pend, ArmsPend &pd, double lam, bool &obsdone) {
   const int n = P.n();
   const double y_t = st.yt;
+  const int j = st.j;
   /* (the caller has generated the next Philox block for this round's
-   * draws: invert, test, Metropolis, moveMass, at most 4 words) */
-  if (start && !st.haveE0) { /* s_j = 0: no absorb test ran at this state */
-#pragma unroll
-    for (int i = 0; i < n; i++) st.E0[i] = pht_exp_neg(P.evals(i) * y_t);
-    st.haveE0 = true;
-    st.haveDen = false;
-  }
+   * draws: invert, test, Metropolis, moveMass, at most 4 words; a new
+   * observation's first absorb test takes one more) */
+  /* a starting lane without E0 is at its observation's first sojourn: the
+   * initial envelope produces E0 from its own vector (ecs_first_E0's rule) */
+  const bool mk = start && !st.haveE0;
   EcsDens<NT> f = ecs_dens(P, st, lam);
   PHT_STAMP(ln, 1);
   double xsamp = 0.0;
   int ainfo = 0;
   bool fin = false;  /* the jump ends this round without an iteration */
   bool big = false;  /* envelope outgrows kRoundCap: general code */
+  obsdone = false;
 
   /* ---- starting lanes: initial envelope (arms(), src/arms.c:226-333) */
   if (start) {
@@ -297,6 +297,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
     xinit[1] = (y_t) / 3.0;
     xinit[2] = xinit[1] * 2.0;
     xinit[3] = y_t - xinit[0];
+    double yv[4];
     if ((xinit[0] <= 0.0) || (xinit[3] >= y_t)) {
       ainfo = 1003;
       fin = true;
@@ -304,10 +305,30 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
       ainfo = 1004;
       fin = true;
     } else {
+      f.init4(xinit, yv, mk, st.E0);
+    }
+    if (mk && fin) ecs_first_E0(P, y_t, lam, st.E0); /* rare: no envelope computed it */
+    st.haveE0 = true;
+    /* a new observation's first absorb test (ecs_try_absorb: the same draw
+     * and arithmetic, after its E0 above) */
+    if (st.fold) {
+      st.fold = false;
+      if (P.s(j) > 0.0) {
+        const double U = dev_u(ln.r);
+        const double den = dev_dot16([&](int i) { return P.QQs(j, i); }, st.E0, n);
+        if (ecs_absorbs(U, P.S(j, j), y_t, P.logs(j), den)) {
+          sk.N(j, j);
+          sk.z(j, y_t);
+          sk.pre(j);
+          obsdone = true;
+          fin = false;
+          ainfo = 0;
+        }
+      }
+    }
+    if (!fin && !obsdone) {
       env.cnt = 9;
       env.sX(0, 0.0);
-      double yv[4];
-      f.init4(xinit, yv);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         env.sX(2 * k + 1, xinit[k]);
@@ -317,6 +338,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
       env.sX(8, y_t);
     }
   }
+  start = start && !obsdone;
   PHT_STAMP(ln, 2);
   /* ---- pending lanes: the update that ends the rejected iteration */
   if (pend) big = (env.cnt + 2 > kRoundCap);

@@ -157,6 +157,19 @@ __device__ __forceinline__ RowV<NT> rv_exp(const RowId<NT> &id, double x) {
   for (int h = 0; h < RowV<NT>::H; h++) r.v[h] = id.sv[h] ? pht_exp_neg(id.lam[h] * x) : 0.0;
   return r;
 }
+/* the lane's slots of E0 at an observation's first sojourn (ecs_first_E0's
+ * rule: (F F) F from the starting points' vector F, or directly) */
+template <int NT>
+__device__ __forceinline__ RowV<NT> rv_first_E0(const RowId<NT> &id, double y_t) {
+  const double a = (y_t) / 1e6, b2 = ((y_t) / 3.0) * 2.0;
+  if (pht_ecs_init_ok(id.lammax, a, y_t - (y_t - a))) {
+    RowV<NT> r = rv_exp(id, y_t - b2);
+#pragma unroll
+    for (int h = 0; h < RowV<NT>::H; h++) r.v[h] = pht_ecs_e0_cube(r.v[h]);
+    return r;
+  }
+  return rv_exp(id, y_t);
+}
 /* the lane's slots of a coefficient row c(i) */
 template <int NT, class Cf>
 __device__ __forceinline__ RowV<NT> rv_coef(const RowId<NT> &id, const Cf &cf) {
@@ -480,8 +493,8 @@ __device__ __forceinline__ bool row_try_absorb(const Par<NT> &P, const RowId<NT>
   } else if (P.s(j) > 0.0) {
     const double y_t = st.yt;
     const double U = dev_u(ln.r);
-    if (!st.haveE0) {
-      st.E0 = rv_exp(id, y_t);
+    if (!st.haveE0) { /* the observation's first sojourn */
+      st.E0 = rv_first_E0(id, y_t);
       st.haveE0 = true;
       st.haveDen = false;
     }
@@ -602,8 +615,8 @@ __device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId<NT> &id,
                                           bool &bigm, ArmsPend &pd) {
   const int rl = id.rl;
   const double y_t = st.yt;
-  if (start && !st.haveE0) {
-    st.E0 = rv_exp(id, y_t);
+  if (start && !st.haveE0) { /* s_j = 0 at the first sojourn */
+    st.E0 = rv_first_E0(id, y_t);
     st.haveE0 = true;
     st.haveDen = false;
   }

@@ -678,6 +678,11 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
         }
         ecs_begin(P, yobs, ln, sk, st);
         have = true;
+        /* its first absorb test runs inside the round, after the initial
+         * envelope whose vector gives its E0 (pht_ecs_round.h) */
+        st.fold = true;
+        need = true;
+        break;
       }
       if (ecs_try_absorb(P, ln, sk, st)) {
         const uint32_t nd = pht_stream_pos(&ln.r);
@@ -737,7 +742,21 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
 #endif
     topup(need || pend);
     PHT_STAMP(ln, 12);
-    ecs_round(P, ln, env, sk, st, need, pend, pd, lam);
+    bool obsdone;
+    ecs_round(P, ln, env, sk, st, need, pend, pd, lam, obsdone);
+    if (obsdone) { /* absorbed at its first test (folded into the round) */
+      const uint32_t nd = pht_stream_pos(&ln.r);
+      if (DEBUG) {
+        a.dbg_flags[pos] = ln.flags;
+        a.dbg_ndraw[pos] = nd;
+      }
+      c_obs++;
+      c_neval += ln.neval;
+      c_flag += ln.flags ? 1u : 0u;
+      c_nd += nd;
+      c_jump += ln.njump;
+      have = false;
+    }
   }
 #ifdef PHT_STAMPS
   /* diagnostic builds: the extra words carry [rounds, 15 stamp slots] */
