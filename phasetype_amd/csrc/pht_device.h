@@ -564,18 +564,21 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
     }
     lammax = lam;
   }
+  /* Elast holds the vector of the most recent evaluation at lastd != 0;
+   * at d = 0 the sum reads E0 itself (no copy: ecs_jump_finish takes E0 for
+   * d = 0 first), so Elast is live only from an evaluation to its use */
   __device__ __forceinline__ double operator()(double d) {
     const int n = P.n();
     const double x = y_t - d;
+    double acc;
     if (haveE0 && d == 0.0) {
-#pragma unroll
-      for (int i = 0; i < n; i++) Elast[i] = E0[i];
+      acc = dev_dot16([&](int i) { return w(i); }, E0, n);
     } else {
 #pragma unroll
       for (int i = 0; i < n; i++) Elast[i] = pht_exp_neg(P.evals(i) * x);
+      acc = dev_dot16([&](int i) { return w(i); }, Elast, n);
+      lastd = d;
     }
-    const double acc = dev_dot16([&](int i) { return w(i); }, Elast, n);
-    lastd = d;
     return pht_log(acc) + Sjj * d;
   }
   /* the four ARMS starting points at once (device spec: pht_ecs_init_ok in
@@ -604,9 +607,11 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
 #pragma unroll
       for (int i = 0; i < n; i++) T[i] = E0[i] * pht_exp_taylor(-P.evals(i) * xinit[0]);
       acc[0] = dev_dot16(Wj, T, n);
+      /* (point y_t - a's vector is not kept: no sojourn ends at d = y_t - a
+       * without a later evaluation, so Elast stays free through the round) */
 #pragma unroll
-      for (int i = 0; i < n; i++) Elast[i] = pht_exp_taylor(P.evals(i) * x3);
-      acc[3] = dev_dot16(Wj, Elast, n);
+      for (int i = 0; i < n; i++) T[i] = pht_exp_taylor(P.evals(i) * x3);
+      acc[3] = dev_dot16(Wj, T, n);
     } else {
       if (E0w && mk) {
 #pragma unroll
@@ -614,14 +619,14 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
       }
 #pragma unroll
       for (int k = 0; k < 4; k++) {
+        double T[PHT_VEC(NT)];
 #pragma unroll
-        for (int i = 0; i < n; i++) Elast[i] = pht_exp_neg(P.evals(i) * (y_t - xinit[k]));
-        acc[k] = dev_dot16(Wj, Elast, n);
+        for (int i = 0; i < n; i++) T[i] = pht_exp_neg(P.evals(i) * (y_t - xinit[k]));
+        acc[k] = dev_dot16(Wj, T, n);
       }
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) yv[k] = pht_log(acc[k]) + Sjj * xinit[k];
-    lastd = xinit[3];
   }
 };
 
@@ -730,11 +735,11 @@ __device__ __forceinline__ void ecs_jump_finish(const Par<NT> &P, Lane &ln, Sink
    * computed them (d = lastd), or d = 0 = the absorb test's; they become
    * the next absorb test's (yt <- x) */
   double *E = st.E0;
-  if (d == f.lastd) {
+  if (d == 0.0) {
+    /* E0 already holds e^{λ_i y_t} = e^{λ_i x} */
+  } else if (d == f.lastd) {
 #pragma unroll
     for (int i = 0; i < n; i++) E[i] = f.Elast[i];
-  } else if (d == 0.0) {
-    /* E0 already holds e^{λ_i y_t} = e^{λ_i x} */
   } else {
 #pragma unroll
     for (int i = 0; i < n; i++) E[i] = pht_exp_neg(P.evals(i) * x);
