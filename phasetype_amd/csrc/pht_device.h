@@ -164,6 +164,12 @@ struct Lane {
 __device__ __forceinline__ double expshift(double y, double y0) {
   return (y - y0 > -2.0 * kYCeil) ? pht_exp_hi(y - y0 + kYCeil) : 0.0;
 }
+/* expshift where y - y0 <= 659 is known (envelope points and hull points
+ * against their own ymax: y <= ymax up to rounding): pht_exp_hi's overflow
+ * clamp cannot act there, so the same value without it */
+__device__ __forceinline__ double expshift_le(double y, double y0) {
+  return (y - y0 > -2.0 * kYCeil) ? pht_exp_core(y - y0 + kYCeil) : 0.0;
+}
 __device__ __forceinline__ double logshift(double y, double y0) { return pht_log(y) + y0 - kYCeil; }
 
 template <class Env>
@@ -224,13 +230,13 @@ __device__ __forceinline__ void arms_cumulate_u(Env &e) {
 #pragma unroll
   for (int k = 1; k < kArmsU; k++) ymax = (k < cnt && ys[k] > ymax) ? ys[k] : ymax;
   e.ymax = ymax;
-  double eyp = expshift(ys[0], ymax);
+  double eyp = expshift_le(ys[0], ymax);
   double cum = 0.;
   e.sCUM(0, cum);
 #pragma unroll
   for (int k = 1; k < kArmsU; k++) {
     const double xp = xs[k - 1], xk = xs[k], yp = ys[k - 1], yk = ys[k];
-    const double eyk = expshift(yk, ymax);
+    const double eyk = expshift_le(yk, ymax);
     const double lin = 0.5 * (eyk + eyp) * (xk - xp);
     const double ex = (PHT_DIV((eyk - eyp), (yk - yp))) * (xk - xp);
     const double a = (xp == xk) ? 0. : ((fabs(yk - yp) < kYEps) ? lin : ex);
@@ -253,12 +259,12 @@ __device__ __forceinline__ void arms_cumulate(Env &e) {
   }
   e.ymax = ymax;
   double xp = e.X(0), yp = e.Y(0);
-  double eyp = expshift(yp, ymax);
+  double eyp = expshift_le(yp, ymax);
   double cum = 0.;
   e.sCUM(0, cum);
   for (int k = 1; k < e.cnt; k++) {
     const double xk = e.X(k), yk = e.Y(k);
-    const double eyk = expshift(yk, ymax);
+    const double eyk = expshift_le(yk, ymax);
     double a;
 #ifdef PHT_AREA_SELECT
     /* branch-free: both cheap forms, then select (same values) */
@@ -319,10 +325,10 @@ __device__ __forceinline__ void arms_invert(Env &e, double prob, WPt &p) {
   const double xl = e.X(q - 1), xr = e.X(q);
   const double yr = e.Y(q);
   if (xl == xr) {
-    p.x = xr; p.y = yr; p.ey = expshift(yr, e.ymax);
+    p.x = xr; p.y = yr; p.ey = expshift_le(yr, e.ymax);
     return;
   }
-  const double yl = e.Y(q - 1), eyl = expshift(yl, e.ymax), eyr = expshift(yr, e.ymax);
+  const double yl = e.Y(q - 1), eyl = expshift_le(yl, e.ymax), eyr = expshift_le(yr, e.ymax);
   if (fabs(yr - yl) < kYEps) {
     if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
       p.x = xl + (PHT_DIV((xr - xl), (eyr - eyl))) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
@@ -333,7 +339,7 @@ __device__ __forceinline__ void arms_invert(Env &e, double prob, WPt &p) {
   } else {
     p.x = xl + (PHT_DIV((xr - xl), (yr - yl))) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
     p.y = (PHT_DIV((p.x - xl), (xr - xl))) * (yr - yl) + yl;
-    p.ey = expshift(p.y, e.ymax);
+    p.ey = expshift_le(p.y, e.ymax);
   }
 }
 

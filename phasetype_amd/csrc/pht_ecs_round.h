@@ -131,13 +131,14 @@ __device__ __forceinline__ void round_cumulate(Env &e, double *cs) {
 #pragma unroll
   for (int k = 1; k < CAP; k++) ymax = (k < cnt && ys[k] > ymax) ? ys[k] : ymax;
   e.ymax = ymax;
-  double eyp = expshift(ys[0], ymax);
+  /* (positions < cnt lie at or below ymax; those beyond are never read) */
+  double eyp = expshift_le(ys[0], ymax);
   double cum = 0.;
   cs[0] = cum;
 #pragma unroll
   for (int k = 1; k < CAP; k++) {
     const double xp = xs[k - 1], xk = xs[k], yp = ys[k - 1], yk = ys[k];
-    const double eyk = expshift(yk, ymax);
+    const double eyk = expshift_le(yk, ymax);
     const double lin = 0.5 * (eyk + eyp) * (xk - xp);
     const double ex = (PHT_DIV((eyk - eyp), (yk - yp))) * (xk - xp);
     const double a = (xp == xk) ? 0. : ((fabs(yk - yp) < kYEps) ? lin : ex);
@@ -152,31 +153,32 @@ __device__ __forceinline__ void round_cumulate(Env &e, double *cs) {
 template <int CAP, class Env>
 __device__ __forceinline__ void round_invert(Env &e, const double *cs, double prob, WPt &p) {
   const int last = e.cnt - 1;
-  double clast = cs[0];
+  /* cum at last and last - 1 (the segment's ends before the scan moves) */
+  double clast = cs[0], cprev = cs[0];
 #pragma unroll
-  for (int k = 1; k < CAP; k++) clast = (k == last) ? cs[k] : clast;
+  for (int k = 1; k < CAP; k++) {
+    clast = (k == last) ? cs[k] : clast;
+    cprev = (k == last) ? cs[k - 1] : cprev;
+  }
   const double u = prob * clast;
-  /* q moves down from last while cum[q-1] > u */
+  /* q moves down from last while cum[q-1] > u; the segment's ends follow */
   int q = last;
+  double cr = clast, cl = cprev;
   bool go = true;
 #pragma unroll
   for (int k = CAP - 2; k >= 1; k--) {
     if (k <= last - 1) {
       go = go && (cs[k] > u);
       q = go ? k : q;
+      cr = go ? cs[k] : cr;
+      cl = go ? cs[k - 1] : cl;
     }
-  }
-  double cr = cs[0], cl = cs[0];
-#pragma unroll
-  for (int k = 1; k < CAP; k++) {
-    cr = (k == q) ? cs[k] : cr;
-    cl = (k == q) ? cs[k - 1] : cl;
   }
   p.pr = q;
   const double prop = PHT_DIV((u - cl), (cr - cl));
   const double xl = e.X(q - 1), xr = e.X(q);
   const double yr = e.Y(q), yl = e.Y(q - 1);
-  const double eyr = expshift(yr, e.ymax);
+  const double eyr = expshift_le(yr, e.ymax);
   /* the point is built in scalars and stored once: assigning p's fields in
    * both branches let the compiler merge them into one store through a
    * selected field address, which put p (and its reloads) in scratch every
@@ -185,7 +187,7 @@ __device__ __forceinline__ void round_invert(Env &e, const double *cs, double pr
   if (xl == xr) {
     px = xr; py = yr; pey = eyr;
   } else {
-    const double eyl = expshift(yl, e.ymax);
+    const double eyl = expshift_le(yl, e.ymax);
     if (fabs(yr - yl) < kYEps) {
       if (fabs(eyr - eyl) > kEYEps * fabs(eyr + eyl))
         px = xl + (PHT_DIV((xr - xl), (eyr - eyl))) * (-eyl + sqrt((1. - prop) * eyl * eyl + prop * eyr * eyr));
@@ -196,7 +198,7 @@ __device__ __forceinline__ void round_invert(Env &e, const double *cs, double pr
     } else {
       px = xl + (PHT_DIV((xr - xl), (yr - yl))) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
       py = (PHT_DIV((px - xl), (xr - xl))) * (yr - yl) + yl;
-      pey = expshift(py, e.ymax);
+      pey = expshift_le(py, e.ymax);
     }
   }
   p.x = px;

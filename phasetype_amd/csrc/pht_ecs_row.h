@@ -346,7 +346,7 @@ __device__ __forceinline__ double row_cumulate(RowEnv &e, int rl, double &ey) {
   }
   const double ymax = mx;
   e.ymax = ymax;
-  const double eyk = expshift(e.y, ymax);
+  const double eyk = expshift_le(e.y, ymax); /* (lanes beyond cnt: never read) */
   ey = eyk;
   const double xp = dpp_pd<dpp_shr(1)>(e.x), yp = dpp_pd<dpp_shr(1)>(e.y), eyp = dpp_pd<dpp_shr(1)>(eyk);
   const double xk = e.x, yk = e.y;
@@ -411,7 +411,7 @@ __device__ __forceinline__ void row_invert(const RowEnv &e, double cum, double e
   } else {
     p.x = xl + (PHT_DIV((xr - xl), (yr - yl))) * (-yl + logshift(((1. - prop) * eyl + prop * eyr), e.ymax));
     p.y = (PHT_DIV((p.x - xl), (xr - xl))) * (yr - yl) + yl;
-    p.ey = expshift(p.y, e.ymax);
+    p.ey = expshift_le(p.y, e.ymax);
   }
 }
 
