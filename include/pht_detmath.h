@@ -518,6 +518,37 @@ PHT_HD int pht_ecs_init_ok(double lammax, double a, double x3) {
  * Error: ~3 ulp plus |lambda y_t| 2^-52 from y_t ~ 3 (y_t - 2b). */
 PHT_HD double pht_ecs_e0_cube(double F) { return (F * F) * F; }
 
+/* W moments (device spec, r03): Wm_k = c_k sum_i W_i lambda_i^k, k = 0..5,
+ * with c_k pht_exp_taylor's coefficients (1, 1, 1/2, 1/3!, 1/4!, 1/5!), so
+ * that sum_i W_i taylor5(lambda_i x) = pht_wmom_eval(Wm, x): the ECS density
+ * at the starting point y_t - a (x = a's image, |lambda| x <= 2^-8) becomes
+ * one degree-5 polynomial per state instead of n Taylor factors and a dot
+ * product per sojourn.  Per-sweep constants (host, resident kernel, oracle
+ * all call this with the same operation order). */
+#define PHT_WMOM 6
+PHT_HD void pht_wmoments(int n, const double *W, long wstride, const double *evals, double *out) {
+  const double c[PHT_WMOM] = {1.0, 1.0, 0.5, 1.6666666666666665741e-01, 4.1666666666666664354e-02,
+                              8.3333333333333332177e-03};
+  for (int k = 0; k < PHT_WMOM; k++) {
+    double acc = 0.0;
+    for (int i = 0; i < n; i++) {
+      double lp = 1.0;
+      for (int m = 0; m < k; m++) lp = lp * evals[i];
+      acc = fma(W[i * wstride], lp, acc);
+    }
+    out[k] = acc * c[k];
+  }
+}
+/* the moments' polynomial at x (Wm_k at Wm[k * stride]) */
+PHT_HD double pht_wmom_eval(const double *Wm, long stride, double x) {
+  double q = Wm[5 * stride];
+  q = fma(q, x, Wm[4 * stride]);
+  q = fma(q, x, Wm[3 * stride]);
+  q = fma(q, x, Wm[2 * stride]);
+  q = fma(q, x, Wm[1 * stride]);
+  return fma(q, x, Wm[0]);
+}
+
 /* Spectral dot product sum_i c_i e_i of the ECS path, in the order every
  * implementation (one lane per observation, or G lanes sharing one) can
  * reproduce: 16 residue slots p_r = c_r e_r (fma with c_{r+16} e_{r+16}

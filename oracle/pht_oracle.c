@@ -194,6 +194,11 @@ int orc_sp_build(orc_sp *sp, int n, const double *S, const double *s, int method
     for (int k = 0; k < n; k++) a = fma(sp->pi[k], sp->Q[k + i * n], a);
     sp->piQ[i] = a;
   }
+  for (int j = 0; j < n; j++) { /* the ECS starting point y_t - a (pht_detmath.h) */
+    double m[PHT_WMOM];
+    pht_wmoments(n, sp->W + j, n, sp->evals, m);
+    for (int k = 0; k < PHT_WMOM; k++) sp->Wm[j + k * n] = m[k];
+  }
   for (int j = 0; j < n; j++) {
     int a = 0, b = 0, c = 0;
     for (int k = 0; k < n; k++) {

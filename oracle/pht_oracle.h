@@ -40,6 +40,7 @@ typedef struct {
   double logs[ORC_MAXN];           /* log(s_j) (s_j > 0)                       */
   double scale[ORC_MAXN];          /* 1/-S_jj                                  */
   double logscale[ORC_MAXN];       /* log(1/-S_jj)                             */
+  double Wm[ORC_MAXN * 6];         /* Wm[j + k n] = pht_wmoments(W[j,.])_k     */
   /* candidate lists (device mode scans only these, in increasing index):
    *   succP[j]  = {k : P[j,k] != 0}          (moveMass, censored jump)
    *   succPf[j] = {k in 0..n : Pfull[j,k] != 0} (MHRS, censored t >= y)

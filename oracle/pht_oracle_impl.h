@@ -603,8 +603,12 @@ static void ORC_FN(ecs_init4)(const double xinit[4], double yv[4], void *vctx) {
       E[2][i] = F;
       E[1][i] = F * F;
       E[0][i] = c->E0[i] * pht_exp_taylor(-sp->evals[i] * xinit[0]);
-      E[3][i] = pht_exp_taylor(sp->evals[i] * x3);
     }
+    /* point y_t - a: the state's W-moment polynomial (pht_wmoments) */
+    yv[3] = ORC_LOG(pht_wmom_eval(sp->Wm + j, n, x3)) + sp->S[j + j * n] * xinit[3];
+    for (int k = 0; k < 3; k++)
+      yv[k] = ORC_LOG(pht_dot16(sp->W + j, n, E[k], n)) + sp->S[j + j * n] * xinit[k];
+    return;
   } else {
     for (int k = 0; k < 4; k++)
       for (int i = 0; i < n; i++) E[k][i] = ORC_EXP_NEG(sp->evals[i] * (y_t - xinit[k]));

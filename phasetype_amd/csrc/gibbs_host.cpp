@@ -315,6 +315,11 @@ static int build_params(int n, const double *S, const double *s, int method, std
     for (int k = 0; k < n; k++) a = fma(d[L.pi + k], Q[k + i * n], a);
     d[L.piQ + i] = a;
   }
+  for (int j = 0; j < n; j++) { /* ECS starting point y_t - a (pht_detmath.h pht_wmoments) */
+    double m[PHT_WMOM];
+    pht_wmoments(n, d + L.W + j, n, d + L.evals, m);
+    for (int k = 0; k < PHT_WMOM; k++) d[L.Wm + j + k * n] = m[k];
+  }
   for (int j = 0; j < n; j++) {
     int a = 0, b = 0, c = 0;
     for (int k = 0; k < n; k++) {

@@ -83,6 +83,7 @@ struct Par {
   __device__ __forceinline__ double V(int i, int j) const { return d[lay().V + i + j * n()]; }
   __device__ __forceinline__ double Q(int i, int j) const { return d[lay().Q + i + j * n()]; }
   __device__ __forceinline__ double Qinv(int i, int j) const { return d[lay().Qinv + i + j * n()]; }
+  __device__ __forceinline__ const PHT_LDS double *Wm(int j) const { return d + lay().Wm + j; } /* stride n() */
   __device__ __forceinline__ int nsuccP(int j) const { return iv[lay().nsuccP + j]; }
   __device__ __forceinline__ int succP(int j, int q) const { return iv[lay().succP + j * n() + q]; }
   __device__ __forceinline__ int nsuccPf(int j) const { return iv[lay().nsuccPf + j]; }
@@ -613,11 +614,18 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
 #pragma unroll
       for (int i = 0; i < n; i++) T[i] = E0[i] * pht_exp_taylor(-P.evals(i) * xinit[0]);
       acc[0] = dev_dot16(Wj, T, n);
-      /* (point y_t - a's vector is not kept: no sojourn ends at d = y_t - a
-       * without a later evaluation, so Elast stays free through the round) */
-#pragma unroll
-      for (int i = 0; i < n; i++) T[i] = pht_exp_taylor(P.evals(i) * x3);
-      acc[3] = dev_dot16(Wj, T, n);
+      /* point y_t - a: sum_i W_i taylor5(lambda_i x3) as the state's W-moment
+       * polynomial (pht_wmoments; no vector) */
+      {
+        const PHT_LDS double *m = P.Wm(j);
+        const int st = n;
+        double q = m[5 * st];
+        q = fma(q, x3, m[4 * st]);
+        q = fma(q, x3, m[3 * st]);
+        q = fma(q, x3, m[2 * st]);
+        q = fma(q, x3, m[1 * st]);
+        acc[3] = fma(q, x3, m[0]);
+      }
     } else {
       if (E0w && mk) {
 #pragma unroll

@@ -215,6 +215,7 @@ struct RowDens {
   RowV<NT> E0; /* e^{lambda_i y_t} */
   RowV<NT> El; /* the most recent evaluation */
   double lastd;
+  const PHT_LDS double *Wm; /* the state's W moments (stride NT) */
   __device__ __forceinline__ double sum(const RowV<NT> &e) const { return rv_dot(id, w, e); }
   __device__ __forceinline__ double operator()(double d) {
     const double x = y_t - d;
@@ -234,20 +235,28 @@ struct RowDens {
       for (int h = 0; h < H; h++) {
         T1.v[h] = F.v[h] * F.v[h];
         T0.v[h] = E0.v[h] * pht_exp_taylor(-id.lam[h] * xinit[0]);
-        El.v[h] = pht_exp_taylor(id.lam[h] * x3);
       }
       acc[2] = sum(F);
       acc[1] = sum(T1);
       acc[0] = sum(T0);
-      acc[3] = sum(El);
+      /* point y_t - a: the state's W-moment polynomial (pht_wmoments) */
+      {
+        const PHT_LDS double *m = Wm;
+        double q = m[5 * NT];
+        q = fma(q, x3, m[4 * NT]);
+        q = fma(q, x3, m[3 * NT]);
+        q = fma(q, x3, m[2 * NT]);
+        q = fma(q, x3, m[1 * NT]);
+        acc[3] = fma(q, x3, m[0]);
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         El = rv_exp(id, y_t - xinit[k]);
         acc[k] = sum(El);
       }
+      lastd = xinit[3];
     }
-    lastd = xinit[3];
   }
 };
 
@@ -622,7 +631,7 @@ __device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId<NT> &id,
   }
   const int j = st.j;
   const RowSucc<NT> su = row_succ<NT>(P, id, j);
-  RowDens<NT> f{id, j, y_t, P.S(j, j), rv_coef(id, [&](int i) { return P.W(j, i); }), st.E0, {}, -1.0};
+  RowDens<NT> f{id, j, y_t, P.S(j, j), rv_coef(id, [&](int i) { return P.W(j, i); }), st.E0, {}, -1.0, P.Wm(j)};
   PHT_STAMP(ln, 1);
   double xsamp = 0.0;
   int ainfo = 0;

@@ -17,6 +17,7 @@
  *   QQ1    Q[j,i] (Q⁻¹1)_i                  phtcdf(e_j)
  *   V      (P_j.ᵀ Q)_i (Q⁻¹1)_i             phtcdf(P_j.)
  *   Q, Qinv eigenvectors and inverse        DCS
+ *   Wm     Wm[j + k n], k < 6: pht_wmoments of row W[j,.]  ECS init point y_t - a
  * int region: candidate lists (increasing index) and their counts
  *   succP[j n + q]      {k : P[j,k] != 0}
  *   succPf[j (n+1) + q] {k in 0..n : Pf[j,k] != 0}
@@ -38,7 +39,7 @@ constexpr int kMaxN = 32;
 struct Layout {
   int n;
   /* f64 offsets (in doubles) */
-  int evals, s, logs, scale, logscale, piQ, pi, S, P, Pf, QQs, W, QQ1, V, Q, Qinv, ndouble;
+  int evals, s, logs, scale, logscale, piQ, pi, S, P, Pf, QQs, W, QQ1, V, Q, Qinv, Wm, ndouble;
   /* int32 offsets (in ints, from the start of the int region) */
   int nsuccP, succP, nsuccPf, succPf, nsuccS, succS, nint;
   PHT_LHD int bytes() const { return ndouble * 8 + nint * 4; }
@@ -64,6 +65,7 @@ PHT_LHD Layout make_layout(int n) {
   L.V = o; o += nn;
   L.Q = o; o += nn;
   L.Qinv = o; o += nn;
+  L.Wm = o; o += 6 * n;
   o += (o & 1); /* keep the int region 16-byte aligned */
   L.ndouble = o;
   int k = 0;

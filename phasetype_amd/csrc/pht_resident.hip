@@ -45,6 +45,16 @@ constexpr int kResMaxM = (kMaxN + 1) * (kMaxN + 1);
  * data in place (finite values; the host reports the error after the run);
  * at init it writes diag(S) and identity vectors instead.
  */
+/* the ECS starting point's W moments from the block's W and evals (as
+ * build_params; W and evals complete before the call) */
+__device__ __forceinline__ void wmoments(int n, const Layout &L, double *dv) {
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    double m[PHT_WMOM];
+    pht_wmoments(n, dv + L.W + j, n, dv + L.evals, m);
+    for (int k = 0; k < PHT_WMOM; k++) dv[L.Wm + j + k * n] = m[k];
+  }
+}
+
 __device__ __forceinline__ void spectral(const ResidentArgs &r, int n, const Layout &L, double *dv) {
   __shared__ double eH[kMaxN * kMaxN], eV[kMaxN * kMaxN], eX[kMaxN * kMaxN], eG[2 * kMaxN * kMaxN];
   __shared__ double eQ[kMaxN * kMaxN], eort[kMaxN], escale[kMaxN], ed[kMaxN], eev[kMaxN], eQs[kMaxN], eQ1[kMaxN];
@@ -69,6 +79,8 @@ __device__ __forceinline__ void spectral(const ResidentArgs &r, int n, const Lay
         dv[L.evals + i] = dv[L.S + i + i * n];
         dv[L.piQ + i] = (i == 0) ? 1.0 : 0.0;
       }
+      __syncthreads();
+      wmoments(n, L, dv);
     }
     return;
   }
@@ -107,6 +119,8 @@ __device__ __forceinline__ void spectral(const ResidentArgs &r, int n, const Lay
     for (int k = 0; k < n; k++) a = fma(dv[L.pi + k], eQ[k + i * n], a);
     dv[L.piQ + i] = a;
   }
+  __syncthreads(); /* W and evals complete */
+  wmoments(n, L, dv);
 }
 
 __global__ void __launch_bounds__(kResThreads) resident_update_kernel(ResidentArgs r, int iter) {

@@ -14,6 +14,7 @@
   detmath exp/log accuracy (< 1 ulp, specials).
 """
 import ctypes as C
+import math
 import os
 import re
 
@@ -121,7 +122,7 @@ def _layout(n):
     o, L = 0, {}
     for name, size in (("evals", n), ("s", n), ("logs", n), ("scale", n), ("logscale", n), ("piQ", n), ("pi", n),
                        ("S", nn), ("P", nn), ("Pf", nn + n), ("QQs", nn), ("W", nn), ("QQ1", nn), ("V", nn),
-                       ("Q", nn), ("Qinv", nn)):
+                       ("Q", nn), ("Qinv", nn), ("Wm", 6 * n)):
         L[name] = (o, size)
         o += size
     o += o & 1
@@ -141,7 +142,7 @@ def _orc_sp_struct(M):
               ("Pfull", d * (M * (M + 1))), ("Q", d * (M * M)), ("Qinv", d * (M * M)), ("evals", d * M),
               ("Qinv_s", d * M), ("Qinv_1", d * M), ("eig_info", i), ("QQs", d * (M * M)), ("W", d * (M * M)),
               ("QQ1", d * (M * M)), ("V", d * (M * M)), ("piQ", d * M), ("logs", d * M), ("scale", d * M),
-              ("logscale", d * M), ("succP", i * (M * M)), ("nsuccP", i * M), ("succPf", i * (M * (M + 1))),
+              ("logscale", d * M), ("Wm", d * (M * 6)), ("succP", i * (M * M)), ("nsuccP", i * M), ("succPf", i * (M * (M + 1))),
               ("nsuccPf", i * M), ("succS", i * (M * M)), ("nsuccS", i * M)]
     return type("orc_sp", (C.Structure,), {"_fields_": fields})
 
@@ -184,7 +185,7 @@ def test_params_block_equals_gpu_spec(lib, orc, n, method):
              ("scale", "scale"), ("logscale", "logscale")]
     if eig:
         pairs += [("evals", "evals"), ("Q", "Q"), ("Qinv", "Qinv"), ("QQs", "QQs"), ("W", "W"), ("QQ1", "QQ1"),
-                  ("V", "V"), ("piQ", "piQ")]
+                  ("V", "V"), ("piQ", "piQ"), ("Wm", "Wm")]
     for mine, theirs in pairs:
         o, size = L[mine]
         want = np.ctypeslib.as_array(getattr(sp, theirs))[:size]
@@ -224,6 +225,35 @@ def test_params_eigensystem_equals_reference(lib, orc, n):
             o, size = L[name]
             want = np.ctypeslib.as_array(getattr(_spview(orc, sp), name))[:size]
             assert np.array_equal(dv[o:o + size], want), (name, seed)
+
+
+@pytest.mark.parametrize("n", [3, 5, 10, 15, 20])
+def test_w_moment_polynomial_matches_taylor_sum(lib, orc, n):
+    """The ECS starting point y_t - a (device spec r03, pht_wmoments): the
+    per-state polynomial sum_k Wm_k x^k equals sum_i W_i taylor5(lambda_i x)
+    for |lambda| x <= 2^-8 within 8 ulp of sum_i |W_i| (both sums cancel
+    alike; extended-precision reference)."""
+    L, _, nbytes, nd = _layout(n)
+    for seed in range(5):
+        S, s = _perturbed(n, 31 * n + seed)
+        buf = np.zeros(nbytes, np.uint8)
+        lib.pht_build_params(n, np.ascontiguousarray(S.reshape(-1, order="F")), s, 2,
+                             buf.ctypes.data_as(C.c_void_p), nbytes)
+        dv = buf[: nd * 8].view(np.float64)
+        ev = dv[L["evals"][0]:L["evals"][0] + n]
+        W = dv[L["W"][0]:L["W"][0] + n * n].reshape(n, n, order="F")
+        Wm = dv[L["Wm"][0]:L["Wm"][0] + 6 * n].reshape(n, 6, order="F")
+        lam = np.abs(ev).max()
+        for x in (0.0, 1e-9 / lam, 2.0 ** -12 / lam, 2.0 ** -8 / lam):
+            for j in range(n):
+                poly = 0.0
+                for k in range(5, -1, -1):
+                    poly = poly * x + Wm[j, k]
+                u = np.longdouble(ev) * np.longdouble(x)
+                tay = sum(u ** k / np.longdouble(math.factorial(k)) for k in range(6))
+                want = float(np.sum(np.longdouble(W[j]) * tay))
+                scale = np.abs(W[j]).sum()
+                assert abs(poly - want) <= 8 * np.finfo(float).eps * scale + 1e-300, (n, seed, x, j)
 
 
 # -------------------------------------------------------------- host stream
