@@ -214,25 +214,32 @@ __device__ __forceinline__ void round_insert(Env &e, const ArmsPend &pd, F &f, L
   /* cnt + 2 <= CAP */
   const int pr = pd.pr;
   const int last = e.cnt - 1;
+  const int qi = ((pr - 1) & 1) ? pr + 1 : pr;
+  const int ql = (qi >= 2) ? qi - 2 : qi - 1;
+  const int qr = (qi + 2 <= last + 2) ? qi + 2 : qi + 1;
+  /* the new point's neighbours, read from the old envelope before the shift
+   * (new position m holds old m - 2 where the shift moves it, else old m;
+   * ql < qi < qr, so neither is the new point): no store -> load wait */
+  auto src = [&](int m) { return (m >= 2 && m - 2 >= pr && m - 2 <= last) ? m - 2 : m; };
+  const double xl = e.X(src(ql)), xr = e.X(src(qr));
   double xs[CAP], ys[CAP];
 #pragma unroll
-  for (int k = 0; k < CAP; k++) {
+  for (int k = 0; k + 2 < CAP; k++) {
     xs[k] = e.X(k);
     ys[k] = e.Y(k);
   }
+  /* positions k + 2 with k in [pr, last] take old k; the others keep their
+   * value (stores only where it moves) */
 #pragma unroll
   for (int k = 0; k + 2 < CAP; k++) {
-    const bool mv = (k >= pr && k <= last);
-    e.sX(k + 2, mv ? xs[k] : xs[k + 2]);
-    e.sY(k + 2, mv ? ys[k] : ys[k + 2]);
+    if (k >= pr && k <= last) {
+      e.sX(k + 2, xs[k]);
+      e.sY(k + 2, ys[k]);
+    }
   }
   e.cnt += 2;
-  const int qi = ((pr - 1) & 1) ? pr + 1 : pr;
   e.sX(qi, pd.px);
   e.sY(qi, pd.py);
-  const int ql = (qi >= 2) ? qi - 2 : qi - 1;
-  const int qr = (qi + 2 <= e.cnt - 1) ? qi + 2 : qi + 1;
-  const double xl = e.X(ql), xr = e.X(qr);
   if (pd.px < (1. - kXEps) * xl + kXEps * xr) {
     const double xn = (1. - kXEps) * xl + kXEps * xr;
     e.sX(qi, xn);
