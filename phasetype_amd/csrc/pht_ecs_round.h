@@ -253,16 +253,21 @@ __device__ __forceinline__ void round_insert(Env &e, const ArmsPend &pd, F &f, L
   }
 }
 
-/* Metropolis step with the scan unrolled over the converged envelope */
+/* Metropolis step with the scan unrolled over the converged envelope; s0/s1
+ * = the envelope's points 0 and 1 (read by the caller ahead of the proposal's
+ * evaluation, so the LDS round trip is off this step's chain): the segment
+ * when X(1) >= xprev, as always for ECS's xprev = 0 */
 template <class Env>
 __device__ __forceinline__ double round_metropolis(const Env &e, const WPt &p, double ynew, double xprev, double yprev,
-                                                   Lane &ln) {
-  int ql = 0;
-  while (e.X(ql + 1) < xprev) ql++;
-  const int qr = ql + 1;
-  const double xql = e.X(ql), yql = e.Y(ql);
-  double w = PHT_DIV((xprev - xql), (e.X(qr) - xql));
-  double zold = yql + w * (e.Y(qr) - yql);
+                                                   double s0x, double s0y, double s1x, double s1y, Lane &ln) {
+  double xql = s0x, yql = s0y, xqr = s1x, yqr = s1y;
+  if (s1x < xprev) { /* (not for ECS) */
+    int ql = 1;
+    while (e.X(ql + 1) < xprev) ql++;
+    xql = e.X(ql); yql = e.Y(ql); xqr = e.X(ql + 1); yqr = e.Y(ql + 1);
+  }
+  double w = PHT_DIV((xprev - xql), (xqr - xql));
+  double zold = yql + w * (yqr - yql);
   double znew = p.y;
   if (yprev < zold) zold = yprev;
   if (ynew < znew) znew = ynew;
@@ -399,7 +404,9 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
     yv = logshift(u, env.ymax);
   }
   PHT_STAMP(ln, 7);
+  double s0x = 0.0, s0y = 0.0, s1x = 0.0, s1y = 0.0; /* Metropolis' segment, loaded ahead */
   if (itr) {
+    s0x = env.X(0); s0y = env.Y(0); s1x = env.X(1); s1y = env.Y(1);
     ynew = f(q.x);
     ln.neval++;
   }
@@ -410,7 +417,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
       pd.it++;
       pend = true;
     } else {
-      xsamp = round_metropolis(env, q, ynew, 0.0, pd.yprev, ln);
+      xsamp = round_metropolis(env, q, ynew, 0.0, pd.yprev, s0x, s0y, s1x, s1y, ln);
       acc = true;
     }
   }
