@@ -348,20 +348,30 @@ template <class Env, class F>
 __device__ __forceinline__ void arms_update(Env &e, const WPt &p, F &f, Lane &ln) {
   if (e.cnt > kArmsNPoint - 2) return;
   const int pr = p.pr;
+  const int last = e.cnt - 1;
+  const int qi = ((pr - 1) & 1) ? pr + 1 : pr;
+  const int ql = (qi >= 2) ? qi - 2 : qi - 1;
+  const int qr = (qi + 2 <= last + 2) ? qi + 2 : qi + 1;
+  /* the new point's neighbours from the old envelope, before the shift's
+   * stores (new position m holds old m - 2 where the shift moves it, else
+   * old m; ql < qi < qr): no store -> load wait (pht_ecs_round.h) */
+  const int sl = (ql >= 2 && ql - 2 >= pr && ql - 2 <= last) ? ql - 2 : ql;
+  const int sr = (qr >= 2 && qr - 2 >= pr && qr - 2 <= last) ? qr - 2 : qr;
+  const double xl = e.X(sl), xr = e.X(sr);
   if (Env::kUnroll && e.cnt <= kArmsU) {
-    /* positions pr..cnt-1 move up by 2: read all, write positions 2..kArmsU+1 */
-    const int last = e.cnt - 1;
-    double xs[kArmsU + 2], ys[kArmsU + 2];
+    /* positions pr..cnt-1 move up by 2 (stores only where a point moves) */
+    double xs[kArmsU], ys[kArmsU];
 #pragma unroll
-    for (int k = 0; k < kArmsU + 2; k++) {
+    for (int k = 0; k < kArmsU; k++) {
       xs[k] = e.X(k);
       ys[k] = e.Y(k);
     }
 #pragma unroll
     for (int k = 0; k < kArmsU; k++) {
-      const bool mv = (k >= pr && k <= last);
-      e.sX(k + 2, mv ? xs[k] : xs[k + 2]);
-      e.sY(k + 2, mv ? ys[k] : ys[k + 2]);
+      if (k >= pr && k <= last) {
+        e.sX(k + 2, xs[k]);
+        e.sY(k + 2, ys[k]);
+      }
     }
   } else {
     for (int k = e.cnt - 1; k >= pr; k--) {
@@ -370,12 +380,8 @@ __device__ __forceinline__ void arms_update(Env &e, const WPt &p, F &f, Lane &ln
     }
   }
   e.cnt += 2;
-  const int qi = ((pr - 1) & 1) ? pr + 1 : pr;
   e.sX(qi, p.x);
   e.sY(qi, p.y);
-  const int ql = (qi >= 2) ? qi - 2 : qi - 1;
-  const int qr = (qi + 2 <= e.cnt - 1) ? qi + 2 : qi + 1;
-  const double xl = e.X(ql), xr = e.X(qr);
   if (p.x < (1. - kXEps) * xl + kXEps * xr) {
     const double xn = (1. - kXEps) * xl + kXEps * xr;
     e.sX(qi, xn);
