@@ -95,14 +95,20 @@ int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double *nu, const
  * block on this context is summed over `nranks` processes by an RCCL
  * all-reduce (uint64, in place) on the context's stream, before its copy to
  * the host; pht_gibbs_run then takes reduce = NULL.  One rank calls
- * pht_rccl_unique_id and broadcasts the 128 bytes; every rank attaches with
- * the same id.  RCCL is loaded at run time (librccl.so.1).  No reference
- * counterpart: the reference is single-process (src/PHT_MCMC_Aslett.c:325-337). */
+ * pht_rccl_unique_id and broadcasts the 128 bytes; every rank first calls
+ * pht_ctx_rccl_prepare (all LOCAL preconditions: RCCL loadable, no
+ * communicator yet, device, staging buffer of max_len words), the ranks agree
+ * on its verdict, and only then every rank attaches with the same id (the
+ * collective ncclCommInitRank).  RCCL is loaded at run time (librccl.so.1).
+ * No reference counterpart: the reference is single-process
+ * (src/PHT_MCMC_Aslett.c:325-337). */
 int pht_rccl_unique_id(unsigned char *id128);
+int pht_ctx_rccl_prepare(pht_ctx *c, int max_len);
 int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id128, int nranks, int rank);
-/* In-place sum of buf[len] (host int64) over the attached communicator, on
- * the context's stream: the all-reduce a sweep runs on its statistics block,
- * exposed so the caller can check it against its own collective. */
+/* In-place sum of buf[len] (host int64, len <= the prepared max_len) over the
+ * attached communicator, on the context's stream: the all-reduce a sweep runs
+ * on its statistics block, exposed so the caller can check it against its own
+ * collective.  Once attached, a rank always enters the collective. */
 int pht_ctx_rccl_allreduce(pht_ctx *c, long long *buf, int len);
 
 /* Device-resident Gibbs chain (opt-in, NON-PARITY):

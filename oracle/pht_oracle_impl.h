@@ -6,8 +6,14 @@
  *
  *   ORC_DEV == 0  "ref" variant: R's random stream, glibc exp/log and the
  *                 reference's own expression/loop order (natural-order
- *                 BLAS), so it is bit-exact with the reference C compiled
- *                 in oracle/_ref (tests/test_oracle_ref.py).
+ *                 BLAS): the reference's algorithm draw for draw.  PARITY
+ *                 UNPINNED: the reference needs R's headers and nmath,
+ *                 absent here, so nothing compiles it; the rounds-1/2
+ *                 stand-in build is retired.  The committed regression
+ *                 vectors tests/golden/g1-g3 (first written by that build,
+ *                 regenerated bit for bit by tools/make_golden.py --check)
+ *                 are the only remaining link to the reference's C
+ *                 (DESIGN.md §2).
  *   ORC_DEV == 1  "dev" variant: the GPU specification — Philox stream per
  *                 observation (include/pht_philox.h), detmath exp/log
  *                 (include/pht_detmath.h), per-sweep precomputed products
@@ -16,7 +22,7 @@
  *                 it bit for bit (tests/test_gpu_parity.py).
  *
  * Both variants share the control flow below, which restates:
- *   LJMA_samplechain_Bladt         src/Simulate_AbsCTMC_gt_Bladt_MHRS.c:151-277
+ *   LJMA_samplechain_Bladt         src/Simulate_AbsCTMC_gt_Bladt_MHRS.c:34-160
  *   LJMA_MHsample_Bladt (per obs)  src/Simulate_AbsCTMC_eq_Bladt_MHRS.c:37-117
  *   LJMA_probAbsorb / ECS_dens /
  *   moveMass / samplechain_Aslett2 src/Simulate_AbsCTMC_eq_Aslett_ECS.c:21-41,120-171,205-373

@@ -42,7 +42,21 @@ CASES = {
     "n15_cens_mhrs": (15, 1500, 0.3, 1, 1, 0x515, 3000),
     "n15_cens_dcs": (15, 1500, 0.3, 4, 1, 0x515, 3000),
     "n20_ecs": (20, 1000, 0.0, 2, 1, 0x520, 3000),
+    # power pair: MHRS with mhit = 1 is biased (the
+    # "current" path is a fresh rejection draw every sweep),
+    # mhit = 5 much less so; on short observations (y on a grid in
+    # [0.45, 0.55]) the two posteriors differ and the harness must tell them
+    # apart (tests/test_posterior.py, tests/test_gpu_posterior.py)
+    "n4_y05_mhrs1": (4, 2000, 0.0, 1, 1, 0, 3000),
+    "n4_y05_mhrs5": (4, 2000, 0.0, 1, 5, 0, 3000),
 }
+# cases whose data is a deterministic grid instead of PH(e1, S) draws
+GRID_DATA = {"n4_y05_mhrs1": (0.45, 0.55), "n4_y05_mhrs5": (0.45, 0.55)}
+
+
+def grid_obs(N: int, lo: float, hi: float):
+    """N exact observations evenly spread over (lo, hi)."""
+    return lo + (hi - lo) * (np.arange(N) + 0.5) / N, np.zeros(N, np.int32)
 
 
 def case_inputs(name):
@@ -50,7 +64,10 @@ def case_inputs(name):
     n, N, cf, method, mhit, seed, _ = CASES[name]
     S, s = bd_exit(n)
     T, theta = bd_exit_structure(n)
-    y, cen = simulate_ph(S, s, N, seed=seed, censor_frac=cf)
+    if name in GRID_DATA:
+        y, cen = grid_obs(N, *GRID_DATA[name])
+    else:
+        y, cen = simulate_ph(S, s, N, seed=seed, censor_frac=cf)
     nu, zeta = 1.0 + 50.0 * theta, np.full(len(theta), 50.0)
     return n, method, mhit, y, cen, T, nu, zeta
 
@@ -84,6 +101,45 @@ def compare(a: dict, b: dict, k: float = K_SIGMA):
         for i in np.nonzero(z > k)[0]:
             bad.append(f"{st}[{i}]: {a[st][i]:.6g} vs {b[st][i]:.6g} (z = {z[i]:.2f})")
     return not bad, worst, bad
+
+
+def _cell_moments(X, chunk: int = 65536):
+    """(mean, variance) per cell of per-observation arrays X [L, ...],
+    accumulated in chunks (integer counts exactly, in int64)."""
+    L = X.shape[0]
+    integer = np.issubdtype(X.dtype, np.integer)
+    s1 = s2 = None
+    for i in range(0, L, chunk):
+        x = np.ascontiguousarray(X[i:i + chunk]).reshape(min(chunk, L - i), -1)
+        x = x.astype(np.int64 if integer else np.float64)
+        a, b = x.sum(0), (x * x).sum(0)
+        s1, s2 = (a, b) if s1 is None else (s1 + a, s2 + b)
+    mean = s1 / L
+    return mean, np.maximum(s2 / L - mean * mean, 0.0)
+
+
+def sweep_zscores(za, Na, zb, Nb):
+    """Per-cell agreement of two step-1 sweeps over the same observations
+    (different random streams): |mean_a - mean_b| / se for every z_k (per
+    observation sojourn totals) and every N_jk (transition counts, diagonal
+    = absorptions), se = sqrt(var_a/L + var_b/L) from the per-observation
+    variances, floored for N at the Poisson level of the pooled mean
+    (sqrt((m_a + m_b)/L)) so rare cells are not over-weighted.  Returns
+    dict(z, N: z-scores; z_se, N_se: the standard errors; z_mean, N_mean:
+    side a's means).  The smallest per-cell bias the 5-sigma bar detects
+    is 5 se."""
+    L = za.shape[0]
+    out = {}
+    for key, A, B in (("z", za, zb), ("N", Na, Nb)):
+        ma, va = _cell_moments(A)
+        mb, vb = _cell_moments(B)
+        se = np.sqrt(va / L + vb / L)
+        if key == "N":
+            se = np.maximum(se, np.sqrt((ma + mb) / L))
+        d = np.abs(ma - mb)
+        out[key] = np.where(se > 0, d / np.where(se > 0, se, 1.0), np.where(d > 0, np.inf, 0.0))
+        out[key + "_se"], out[key + "_mean"] = se, ma
+    return out
 
 
 def pack(prefix: str, summ: dict) -> dict:

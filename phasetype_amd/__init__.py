@@ -50,7 +50,7 @@ EXPORTS = [
     "pht_build_params", "pht_ctx_create", "pht_ctx_destroy", "pht_ctx_set_obs", "pht_ctx_sweep",
     "pht_ctx_sweep_debug", "pht_ctx_last_kernel_ms", "pht_ctx_flagged_obs", "pht_ctx_set_global_count", "pht_gibbs_run",
     "pht_gibbs_run_resident",
-    "pht_gibbs_run_chains", "pht_rccl_unique_id", "pht_ctx_attach_rccl", "pht_ctx_rccl_allreduce",
+    "pht_gibbs_run_chains", "pht_rccl_unique_id", "pht_ctx_rccl_prepare", "pht_ctx_attach_rccl", "pht_ctx_rccl_allreduce",
 ]
 
 
@@ -107,6 +107,7 @@ def load(build_if_needed: bool = True) -> C.CDLL:
     L.pht_gibbs_run_chains.argtypes = [C.POINTER(C.c_void_p), C.c_int, _up, C.c_int, C.c_int, C.c_int, _dp, _dp,
                                        _ip, _dp, C.c_int, _dp, _dp, C.POINTER(C.c_double)]
     L.pht_rccl_unique_id.argtypes = [C.c_void_p]
+    L.pht_ctx_rccl_prepare.argtypes = [C.c_void_p, C.c_int]
     L.pht_ctx_attach_rccl.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_int]
     L.pht_ctx_rccl_allreduce.argtypes = [C.c_void_p, _lp, C.c_int]
     L.LJMA_Gibbs.argtypes = [_ip, _ip, _ip, _ip, _ip, _dp, _dp, _ip, _dp, _dp, _ip, _ip, _dp, _ip, _dp]
@@ -208,11 +209,19 @@ class Sweeper:
         if self.L.pht_ctx_set_global_count(self.ctx, int(total)) != 0:
             raise _err(self.L)
 
+    def rccl_prepare(self, max_len: int = 256) -> None:
+        """Local preconditions of attach_rccl / rccl_allreduce (RCCL loadable,
+        no communicator yet, device, a staging buffer of max_len words):
+        pht_ctx_rccl_prepare.  Ranks agree on it before anyone attaches."""
+        if self.L.pht_ctx_rccl_prepare(self.ctx, int(max_len)) != 0:
+            raise _err(self.L)
+
     def attach_rccl(self, uid: bytes, nranks: int, rank: int) -> None:
         """Sum every sweep's statistics block over ``nranks`` processes with
-        an RCCL all-reduce on this shard's stream (pht_ctx_attach_rccl);
-        ``uid`` = rccl_unique_id() of one rank, the same on all.  gibbs()
-        then needs no ``reduce``."""
+        an RCCL all-reduce on this shard's stream (pht_ctx_attach_rccl, the
+        collective ncclCommInitRank); ``uid`` = rccl_unique_id() of one rank,
+        the same on all, after rccl_prepare() on every rank.  gibbs() then
+        needs no ``reduce``."""
         if len(uid) != RCCL_ID_BYTES:
             raise ValueError(f"RCCL unique id must be {RCCL_ID_BYTES} bytes, got {len(uid)}")
         if self.L.pht_ctx_attach_rccl(self.ctx, uid, nranks, rank) != 0:

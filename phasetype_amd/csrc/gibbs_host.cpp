@@ -396,6 +396,8 @@ struct pht_ctx {
   long long flagged = 0; /* flagged observation-sweeps of the last Gibbs run (node-wide) */
   long long global_count = -1; /* observations over all shards (pht_ctx_set_global_count) */
   ncclComm_t comm = nullptr; /* pht_ctx_attach_rccl: stats summed over ranks on `stream` */
+  long long *d_rccl = nullptr; /* pht_ctx_rccl_prepare: staging buffer of pht_ctx_rccl_allreduce */
+  int rccl_cap = 0;
   bool stats_zero = false;   /* d_stats zeroed on `stream` after the last sweep's copy */
   hipEvent_t evd = nullptr;  /* the statistics copy to the host is done */
 };
@@ -688,13 +690,19 @@ extern "C" int pht_rccl_unique_id(unsigned char *id) {
   return 0;
 }
 
-extern "C" int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id, int nranks, int rank) {
-  if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) {
-    set_err("pht_ctx_attach_rccl: need a context, a unique id and 0 <= rank < nranks");
+/* Every local precondition of pht_ctx_attach_rccl and pht_ctx_rccl_allreduce,
+ * checked BEFORE any rank enters a collective: RCCL loadable, no communicator
+ * attached yet, the device selectable, and the staging buffer of the
+ * all-reduce self-test (max_len int64 words) allocated.  The caller agrees on
+ * the verdict across ranks first (phasetype_amd/dist.py attach_rccl), so a
+ * rank that fails here cannot leave its peers waiting in ncclCommInitRank. */
+extern "C" int pht_ctx_rccl_prepare(pht_ctx *c, int max_len) {
+  if (!c || max_len < 1) {
+    set_err("pht_ctx_rccl_prepare: need a context and max_len >= 1");
     return -1;
   }
   if (c->comm) {
-    set_err("pht_ctx_attach_rccl: a communicator is already attached");
+    set_err("pht_ctx_rccl_prepare: a communicator is already attached");
     return -1;
   }
   if (!rccl().ok) {
@@ -702,9 +710,37 @@ extern "C" int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id, int nran
     return -1;
   }
   if (hipSetDevice(c->device) != hipSuccess) {
-    set_err("pht_ctx_attach_rccl: device %d", c->device);
+    set_err("pht_ctx_rccl_prepare: device %d", c->device);
     return -1;
   }
+  if (c->d_rccl && c->rccl_cap < max_len) {
+    (void)hipFree(c->d_rccl);
+    c->d_rccl = nullptr;
+    c->rccl_cap = 0;
+  }
+  if (!c->d_rccl) {
+    if (hipMalloc(&c->d_rccl, sizeof(long long) * (size_t)max_len) != hipSuccess) {
+      c->d_rccl = nullptr;
+      set_err("pht_ctx_rccl_prepare: no device memory for %d words", max_len);
+      return -1;
+    }
+    c->rccl_cap = max_len;
+  }
+  return 0;
+}
+
+/* The collective step only: ncclCommInitRank with the broadcast id.  Needs
+ * pht_ctx_rccl_prepare first (agreed across ranks). */
+extern "C" int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id, int nranks, int rank) {
+  if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) {
+    set_err("pht_ctx_attach_rccl: need a context, a unique id and 0 <= rank < nranks");
+    return -1;
+  }
+  if (c->comm || !c->d_rccl || !rccl().ok) {
+    set_err("pht_ctx_attach_rccl: call pht_ctx_rccl_prepare first (and agree on it across ranks)");
+    return -1;
+  }
+  (void)hipSetDevice(c->device);
   ncclUniqueId u;
   memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
   ncclComm_t comm = nullptr;
@@ -720,22 +756,22 @@ extern "C" int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id, int nran
 /* in-place sum of a host int64 vector over the context's communicator, on its
  * stream (the same all-reduce a sweep runs on its statistics block): the
  * attach-time self-test of phasetype_amd/dist.py compares it with
- * torch.distributed's sum */
+ * torch.distributed's sum.  The staging buffer comes from
+ * pht_ctx_rccl_prepare; once the communicator exists this rank always enters
+ * the all-reduce, even when its upload failed (the error is reported after
+ * the collective), so its peers are never left waiting. */
 extern "C" int pht_ctx_rccl_allreduce(pht_ctx *c, long long *buf, int len) {
-  if (!c || !c->comm || !buf || len < 1) {
-    set_err("pht_ctx_rccl_allreduce: need a context with an RCCL communicator and a buffer");
+  if (!c || !c->comm || !buf || len < 1 || len > c->rccl_cap) {
+    set_err("pht_ctx_rccl_allreduce: need a context with an RCCL communicator and 1 <= len <= the prepared size");
     return -1;
   }
-  HIPCHK(hipSetDevice(c->device));
-  void *d = nullptr;
-  HIPCHK(hipMalloc(&d, sizeof(long long) * len));
-  hipError_t e = hipMemcpyAsync(d, buf, sizeof(long long) * len, hipMemcpyHostToDevice, c->stream);
-  ncclResult_t r = ncclSuccess;
-  if (e == hipSuccess) r = rccl().allReduce(d, d, (size_t)len, ncclUint64, ncclSum, c->comm, c->stream);
+  (void)hipSetDevice(c->device);
+  hipError_t e = hipMemcpyAsync(c->d_rccl, buf, sizeof(long long) * len, hipMemcpyHostToDevice, c->stream);
+  const ncclResult_t r = rccl().allReduce(c->d_rccl, c->d_rccl, (size_t)len, ncclUint64, ncclSum, c->comm, c->stream);
   if (e == hipSuccess && r == ncclSuccess)
-    e = hipMemcpyAsync(buf, d, sizeof(long long) * len, hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess && r == ncclSuccess) e = hipStreamSynchronize(c->stream);
-  (void)hipFree(d);
+    e = hipMemcpyAsync(buf, c->d_rccl, sizeof(long long) * len, hipMemcpyDeviceToHost, c->stream);
+  const hipError_t es = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = es;
   if (r != ncclSuccess) {
     set_err("RCCL all-reduce failed: %s", rccl().errStr(r));
     return -1;
@@ -809,6 +845,7 @@ extern "C" void pht_ctx_destroy(pht_ctx *c) {
   if (c->evj) (void)hipEventDestroy(c->evj);
   if (c->evd) (void)hipEventDestroy(c->evd);
   if (c->comm) rccl_destroy(c->comm);
+  if (c->d_rccl) (void)hipFree(c->d_rccl);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -917,7 +954,9 @@ static long exact_rowk(const pht_ctx *c) {
 
 /* UNIF: size (and grow) the context's table for this sweep's parameters
  * (c->h_params): the shard's largest lam = mu y with a Poisson margin
- * (pht_unif.h); observations beyond it are flagged, never wrong */
+ * (pht_unif.h).  Beyond kUnifMaxK rows or lam > kUnifMaxLam an observation
+ * cannot be sampled exactly: it is counted in kXUnifCap and gibbs_run fails
+ * the sweep */
 static int unif_prepare(pht_ctx *c, SweepArgs &a) {
   const Layout L = make_layout(c->n);
   const double *S = reinterpret_cast<const double *>(c->h_params) + L.S;
@@ -1338,6 +1377,14 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
       if (!first_flagged) first_flagged = iter;
       flagged += fl;
     }
+    /* UNIF observations beyond the table or the lam cap carry a path that is
+     * not a draw of the target law (pht_unif.h): an error, not a warning */
+    if (xw[kXUnifCap] > 0) {
+      set_err("sweep %d: %lld UNIF observations need more than %d uniformisation steps or mu*y > %g (the largest "
+              "exit rate times the largest observation); their paths would be wrong: rescale the data",
+              iter, xw[kXUnifCap], kUnifMaxK, kUnifMaxLam);
+      return -1;
+    }
 #endif
     for (int k = 0; k < n; k++) z[k] = ldexp((double)tot[k], -zexp);
     G.update(R, iter, z.data(), tot.data() + 2 * n);
@@ -1645,7 +1692,9 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
   a.mcnt = c->d_mcnt;
   if (disp == kMethodUNIF) {
     /* table capacity: twice the prior mode's largest exit rate (the device
-     * sizes each sweep's table from its own mu within it; rows beyond flag) */
+     * sizes each sweep's table from its own mu within it).  A chain whose mu
+     * drifts past that needs rows beyond the capacity: those observations
+     * are counted in kXUnifCap and the update kernel stops the run (err 16) */
     double mu0 = 0.0;
     {
       std::vector<double> rowsum(n1, 0.0);
@@ -1673,7 +1722,16 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
     a.utab = c->d_utab;
   }
   HIPCHK(hipEventRecord(c->ev0, st));
+  int early = 0; /* the error word, polled every kErrPoll sweeps */
+  constexpr int kErrPoll = 256;
   for (int iter = 1; iter < it; iter++) {
+    if (iter % kErrPoll == 0) {
+      /* a failed sweep (e.g. the eigensystem) makes the update kernels
+       * return at entry; stop enqueueing instead of running to `it` */
+      HIPCHK(hipMemcpyAsync(&early, berr.p, sizeof early, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (early) break;
+    }
     a.sweep = (uint32_t)iter;
     if ((c->count > 0 || disp == kMethodUNIF) && ctx_launch(c, a, false)) return -1;
     if (c->comm) {
@@ -1698,11 +1756,14 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
   if (kernel_ms_total) *kernel_ms_total = ms;
   c->flagged = (long long)fl;
   if (err) {
-    set_err("resident chain: %s%s%s%s", (err & 1) ? "a sweep did not sample every observation; " : "",
+    set_err("resident chain: %s%s%s%s%s", (err & 1) ? "a sweep did not sample every observation; " : "",
             (err & 2) ? "the fixed-point z sums overflowed (pass a smaller zexp); " : "",
             (err & 4) ? "a Gamma draw failed (non-finite shape/scale or the rejection cap); " : "",
             (err & 8) ? "the eigensystem failed (complex eigenvalues, no QR convergence or singular eigenvectors:"
-                        " the uniformisation sampler, method 8, needs none)" : "");
+                        " the uniformisation sampler, method 8, needs none); " : "",
+            (err & 16) ? "UNIF observations needed more uniformisation steps than the table sized from the start "
+                         "(twice its largest exit rate) holds, or mu*y > 1300: the chain's rates drifted far above "
+                         "the start (start nearer the posterior, or use the host loop, which sizes every sweep)" : "");
     return -1;
   }
   if (fl)

@@ -20,6 +20,7 @@ constexpr int kMhrsCounters = 16;
 /* UNIF per-sweep table in global memory (pht_unif.h):
  * [mu, rinv, K, 0][invk K+1][ax K+1][ac K+1][A (K+1) x n] */
 constexpr int kUnifMaxK = 2047; /* last row index (LDS: 3 (K+1) doubles per block) */
+constexpr double kUnifMaxLam = 1300.0; /* w_0 = 2^-1000 keeps every Poisson weight finite below this */
 constexpr long unif_tab_doubles(int n, int K) { return 4 + 3L * (K + 1) + (long)(K + 1) * n; }
 
 struct SweepArgs {

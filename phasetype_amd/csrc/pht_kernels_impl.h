@@ -1230,7 +1230,11 @@ __device__ __forceinline__ void unif_table_body(const SweepArgs &a) {
     hdr[0] = mu;
     hdr[1] = 1.0 / mu;
     /* rows: the shard's largest lam with a Poisson margin, within the
-     * capacity a.uK (the host's sizing; rows beyond it flag, never bias) */
+     * capacity a.uK (the host's sizing).  An observation that needs rows
+     * beyond it (or lam > kUnifMaxLam) is sampled from a truncated Poisson
+     * sum or a placeholder path, i.e. WRONG: it sets kFlagUnifCap, counted
+     * in the statistics' kXUnifCap word, and the host loop / resident
+     * update turn any such count into an error */
     const double lmax = mu * a.uymax;
     const double kd = ceil(lmax + 14.0 * sqrt(lmax) + 64.0);
     Ksh = (kd < (double)a.uK) ? (int)kd : a.uK;
@@ -1339,7 +1343,7 @@ __device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsi
   U.mu = T[0];
   U.rinv = T[1];
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
-  unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
+  unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0, c_ucap = 0;
   for (;;) {
     const long p = claim_pos(__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), blk, nblk);
     if (p >= a.count) break;
@@ -1362,6 +1366,7 @@ __device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsi
     c_obs++;
     c_neval += ln.neval;
     c_flag += ln.flags ? 1u : 0u;
+    c_ucap += (ln.flags & kFlagUnifCap) ? 1u : 0u;
     c_nd += nd;
     c_jump += ln.njump;
   }
@@ -1370,6 +1375,7 @@ __device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsi
   lds_add(&xc[2], (unsigned long long)c_flag);
   lds_add(&xc[3], (unsigned long long)c_nd);
   lds_add(&xc[4], (unsigned long long)c_jump);
+  if (c_ucap) lds_add(&xc[kXUnifCap], (unsigned long long)c_ucap);
   __syncthreads();
   flush_stats(a.stats, zq, Bc, Nc, xc, n);
 }

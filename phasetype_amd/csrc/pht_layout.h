@@ -85,12 +85,13 @@ PHT_LHD Layout make_layout(int n) {
  *   [n, 2n)         B    start-state counts
  *   [2n, 2n+n^2)    N    N[i + j n] transitions i->j, diagonal = absorb-from
  *   then kStatExtra counters: obs processed, ARMS density evals, obs with
- *   flags, uniforms drawn, jumps, Brent CDF evals, 2 spare, and 8 cycle
+ *   flags, uniforms drawn, jumps, Brent CDF evals, UNIF cap hits, 1 spare, and 8 cycle
  *   counters filled only by diagnostic PHT_STAMPS builds */
 constexpr int kStatExtra = 16; /* [8..15]: per-phase cycle stamps (PHT_STAMPS builds) */
 /* extra-word indices read by the host (gibbs_host.cpp) */
 constexpr int kXObs = 0;       /* observations processed: must equal the shard's count */
 constexpr int kXFlagged = 2;   /* observations that hit a cap or guard */
+constexpr int kXUnifCap = 6;   /* UNIF observations past the Poisson table / lam cap: the sweep is an error */
 constexpr int kXOverflow = 15; /* fixed-point z accumulators crossed 2^63 (never in PHT_STAMPS builds) */
 PHT_LHD int stats_len(int n) { return 2 * n + n * n + kStatExtra; }
 

@@ -129,6 +129,9 @@ __global__ void __launch_bounds__(kResThreads) resident_update_kernel(ResidentAr
   const int n = r.n, n1 = n + 1, m = r.m, tid = threadIdx.x;
   const int sl = stats_len(n);
   const unsigned long long *st = r.stats;
+  /* a failed earlier sweep: stop updating (the host polls the error word and
+   * stops enqueueing; the remaining sweeps are wasted, never reported) */
+  if (!r.init && __hip_atomic_load(r.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   __syncthreads();
   if (!r.init) {
     if (tid == 0) {
@@ -136,6 +139,7 @@ __global__ void __launch_bounds__(kResThreads) resident_update_kernel(ResidentAr
       if (r.expect >= 0 && (long long)xw[kXObs] != r.expect) atomicOr(r.err, 1);
       if (xw[kXOverflow] != 0ull) atomicOr(r.err, 2);
       if (xw[kXFlagged] != 0ull) atomicAdd(r.flagged, xw[kXFlagged]);
+      if (xw[kXUnifCap] != 0ull) atomicOr(r.err, 16);
     }
     for (int k = tid; k < m; k += blockDim.x) {
       long long nsum = 0;

@@ -48,18 +48,23 @@
  *     succPf (one word; an overrun takes the last candidate, flag 1), until
  *     absorption.
  * Draw order: U1 (k*), U2 (j*), [U time, U state] x k*, then the censored
- * continuation.  Flags: kFlagUnifCap (table end, lam cap, zero weights).
+ * continuation.  Flags: kFlagUnifCap (table end, lam cap, zero weights): the
+ * observation's path is then NOT a draw of the target law (a truncated
+ * Poisson sum, or a placeholder path z(0) = y absorbed from state 0), so a
+ * sweep with any such observation is an error (statistics word kXUnifCap;
+ * gibbs_host.cpp fails the run, the resident update sets err bit 16).
  */
 #ifndef PHT_UNIF_H
 #define PHT_UNIF_H
 
 #include "pht_device.h"
+#include "pht_kernels.h"
 
 namespace pht {
 
-constexpr int kFlagUnifCap = 64;      /* UNIF: Poisson table end, lam cap or zero weights */
-constexpr double kUnifMaxLam = 1300.0; /* w_0 = 2^-1000 keeps every weight finite below this */
-/* kUnifMaxK and unif_tab_doubles: pht_kernels.h (the host sizes the table) */
+constexpr int kFlagUnifCap = 64;      /* UNIF: Poisson table end, lam cap or zero weights (an error) */
+/* kUnifMaxK, kUnifMaxLam and unif_tab_doubles: pht_kernels.h (the host sizes
+ * the table and reports the cap) */
 
 template <class APtr>
 struct UnifTab {

@@ -88,6 +88,16 @@ def attach_rccl(sweeper, dist, device: str, n_words: int = 256) -> bool:
         dist.all_reduce(v, op=dist.ReduceOp.MIN)
         return bool(v.item())
 
+    # local preconditions first (RCCL loadable, device, no communicator yet,
+    # the self-test's staging buffer): a rank failing them must not enter
+    # ncclCommInitRank, where its peers would wait for it forever
+    try:
+        sweeper.rccl_prepare(n_words)
+        prepared = True
+    except Exception:  # noqa: BLE001 - reported through the verdict
+        prepared = False
+    if not agree(prepared):
+        return False
     t = torch.zeros(RCCL_ID_BYTES + 1, dtype=torch.uint8, device=device)  # id + "id made" byte
     if dist.get_rank() == 0:
         try:

@@ -115,3 +115,38 @@ def test_resident_guards(gpu):
     with pytest.raises(P.PhaseTypeError, match="did not sample every observation"):
         sw.gibbs_resident(5, 8, nu, zeta, T, Cm, P.zexp_for(y))
     sw.close()
+
+
+def test_unif_cap_is_an_error(gpu):
+    """UNIF observations the uniformisation table cannot sample exactly (rows
+    beyond its capacity, or mu*y > 1300) carry a path that is not a draw of
+    the target law (pht_unif.h): both loops fail the run instead of warning.
+    Resident: the table is sized from the start (twice its largest exit
+    rate, 2.8 -> 498 rows for y = 40); a strong prior at 10x the start's
+    rates pulls the chain's rates (and the rows y = 40 needs) past it within
+    a few sweeps.  The host loop sizes every sweep's table from its own
+    rates, so the same run is fine there; it fails on one observation with
+    mu*y > 1300."""
+    n = 4
+    T, theta = bd_exit_structure(n)
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 200, seed=5)
+    y[0] = 40.0
+    m = len(theta)
+    nu, zeta, Cm = 1 + 5000 * theta, np.full(m, 500.0), np.ones(T.shape)
+    sw = P.Sweeper(n, 8, 1)
+    sw.set_obs(y, cen)
+    with pytest.raises(P.PhaseTypeError, match="UNIF observations needed more"):
+        sw.gibbs_resident(40, 8, nu, zeta, T, Cm, P.zexp_for(y), start=theta)
+    P.set_seed(3)
+    ok = sw.gibbs(40, 8, nu, zeta, T, Cm, P.zexp_for(y), start=theta)
+    assert np.all(np.isfinite(ok)) and sw.flagged_obs == 0
+    assert ok[-1].max() > 5 * theta.max()  # the rates did move far past the start
+    sw.close()
+    yb = y.copy()
+    yb[1] = 1300.0 / 2.8 + 50.0  # mu = 2.8 for BD-exit(4) at the prior mode: lam > 1300
+    sw = P.Sweeper(n, 8, 1)
+    sw.set_obs(yb, cen)
+    with pytest.raises(P.PhaseTypeError, match="UNIF observations need more"):
+        sw.gibbs(3, 8, 1 + 50 * theta, np.full(m, 50.0), T, Cm, P.zexp_for(yb))
+    sw.close()

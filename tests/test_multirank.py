@@ -93,10 +93,17 @@ class _FakeSweeper:
     here): attach fails on the ranks listed, the library all-reduce is
     never reached."""
 
-    def __init__(self, fail_attach):
+    def __init__(self, fail_attach, fail_prepare=False):
         self.fail_attach = fail_attach
+        self.fail_prepare = fail_prepare
+        self.attach_called = False
+
+    def rccl_prepare(self, max_len):
+        if self.fail_prepare:
+            raise RuntimeError("librccl.so.1 could not be loaded (fake)")
 
     def attach_rccl(self, uid, world, rank):
+        self.attach_called = True
         if self.fail_attach:
             raise RuntimeError("ncclCommInitRank failed (fake)")
 
@@ -120,16 +127,22 @@ def _attach_worker(rank, world, port, mode):
                 raise RuntimeError("no RCCL (fake)")
             P.rccl_unique_id = boom
             sw = _FakeSweeper(False)
+        elif mode == "prepare_fails_on_one_rank":  # a local precondition fails on the last rank
+            P.rccl_unique_id = lambda: bytes(P.RCCL_ID_BYTES)
+            sw = _FakeSweeper(False, fail_prepare=rank == world - 1)
         else:  # the communicator fails on the last rank only
             P.rccl_unique_id = lambda: bytes(P.RCCL_ID_BYTES)
             sw = _FakeSweeper(rank == world - 1)
         assert D.attach_rccl(sw, dist, "cpu") is False
+        if mode == "prepare_fails_on_one_rank":
+            # nobody may enter the collective ncclCommInitRank
+            assert not sw.attach_called
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["no_id", "attach_fails_on_one_rank"])
+@pytest.mark.parametrize("mode", ["no_id", "prepare_fails_on_one_rank", "attach_fails_on_one_rank"])
 def test_attach_rccl_failures_fall_back_on_every_rank(mode):
     """bench.py's in-library RCCL reduce: a failure on any rank (no RCCL id
     on rank 0, a communicator that fails on one rank) must return False on

@@ -42,6 +42,44 @@ def test_harness_detects_a_shifted_posterior(orc):
     assert not ok and worst > 8.0, worst
 
 
+@pytest.mark.parametrize("mhit", [1, 5])
+def test_chain_harness_tells_mhrs_mhit_apart(orc, mhit):
+    """Power against a subtle reference effect: MHRS
+    with mhit = 1 is biased.  The device-spec chain at
+    mhit = k must match the reference's mhit = k posterior and fail the
+    other one, on y in [0.45, 0.55]."""
+    d = np.load(GOLD)
+    got = PO.summarize(_dev_chain(orc, f"n4_y05_mhrs{mhit}", 2000))
+    ok, worst, bad = PO.compare(got, PO.unpack(d, f"n4_y05_mhrs{mhit}"))
+    assert ok, (worst, bad[:5])
+    ok, worst, _ = PO.compare(got, PO.unpack(d, f"n4_y05_mhrs{6 - mhit}"))
+    assert not ok and worst > 8.0, worst
+
+
+def test_sweep_harness_tells_mhrs_mhit_apart(orc):
+    """The per-cell sweep comparison (PO.sweep_zscores, used at full size in
+    test_gpu_fullsize.py): the reference's MHRS at mhit = 1 against itself
+    (another stream) and against the device spec passes; against mhit = 5 it
+    fails (3.8e-2 in E[z] at y = 0.5)."""
+    from phasetype_amd.synth import bd_exit
+
+    S, s = bd_exit(4)
+    y, cen = PO.grid_obs(30000, 0.45, 0.55)
+    orc.set_seed(1)
+    a = orc.ref_sweep(1, S, s, y, cen, mhit=1)
+    orc.set_seed(2)
+    b = orc.ref_sweep(1, S, s, y, cen, mhit=1)
+    orc.set_seed(3)
+    c = orc.ref_sweep(1, S, s, y, cen, mhit=5)
+    dv = orc.dev_sweep(1, S, s, y, cen, mhit=1, key=(5, 6))
+    zd = dv["zq"] * 2.0 ** -dv["zexp"]
+    for other_z, other_N in ((b["z"], b["N"]), (zd, dv["N"])):
+        zs = PO.sweep_zscores(a["z"], a["N"], other_z, other_N)
+        assert max(zs["z"].max(), zs["N"].max()) < PO.K_SIGMA, (zs["z"], zs["N"])
+    zs = PO.sweep_zscores(a["z"], a["N"], c["z"], c["N"])
+    assert max(zs["z"].max(), zs["N"].max()) > 3 * PO.K_SIGMA
+
+
 def test_reference_summaries_are_complete():
     d = np.load(GOLD)
     for name, case in PO.CASES.items():
