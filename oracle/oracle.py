@@ -125,6 +125,7 @@ class OracleLib:
         L.orc_eig_refine.argtypes = [C.c_int, _dp, _dp, _dp, _dp, _dp, _dp]
         L.orc_eig_fallback_count.restype = C.c_long
         L.orc_set_dcs_brent.argtypes = [C.c_int]
+        L.orc_set_bridge.argtypes = [C.c_int, C.c_int]
 
     def set_seed(self, seed: int) -> None:
         self.lib.orc_set_seed(seed & 0xFFFFFFFF)
@@ -205,6 +206,13 @@ class OracleLib:
         """dev variant's DCS root finder: Find02's Brent search (on) or the
         device spec's default safeguarded Halley iteration (off)."""
         self.lib.orc_set_dcs_brent(1 if on else 0)
+
+    def set_bridge(self, mhrs: bool = False, dcs: bool = False) -> None:
+        """dev variant's bridge modes (PHT_MHRS=bridge / PHT_DCS=bridge on the
+        device): MHRS's / DCS's path law sampled exactly by the
+        uniformisation sampler (pht_unif.h ulaw 1 / 2) instead of the
+        rejection search / Hobolth's sampler."""
+        self.lib.orc_set_bridge(1 if mhrs else 0, 1 if dcs else 0)
 
     def eig(self, S):
         """The device-resident chain's eigensystem (include/pht_eigen.h):

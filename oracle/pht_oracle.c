@@ -39,6 +39,12 @@ double orc_norm_rand(void) { return pht_rs_norm_rand(&g_rs); }
 static int orc_dcs_brent = 0;
 void orc_set_dcs_brent(int on) { orc_dcs_brent = on; }
 
+/* dev variant's bridge modes (PHT_MHRS=bridge / PHT_DCS=bridge on the
+ * device): MHRS's / DCS's path law sampled by the uniformisation sampler
+ * (phasetype_amd/csrc/pht_unif.h, ulaw 1 / 2) */
+static int orc_bridge_mhrs = 0, orc_bridge_dcs = 0;
+void orc_set_bridge(int mhrs, int dcs) { orc_bridge_mhrs = mhrs; orc_bridge_dcs = dcs; }
+
 /* ------------------------------------------------------------ variants */
 #define ORC_DEV 0
 #define ORC_FN(x) orcR_##x
@@ -258,7 +264,7 @@ int orc_unif_K(const orc_sp *sp, double ymax) {
   return (int)(isfinite(kd) && kd < ORC_UNIF_MAXK ? kd : ORC_UNIF_MAXK);
 }
 
-void orc_unif_table(const orc_sp *sp, int K, double *T) {
+void orc_unif_table(const orc_sp *sp, int K, double *T, int ulaw) {
   const int n = sp->n;
   double mu = 0.0;
   for (int i = 0; i < n; i++) {
@@ -295,8 +301,10 @@ void orc_unif_table(const orc_sp *sp, int K, double *T) {
   for (int k = 0; k <= K; k++) {
     double sx = 0.0, sc = 0.0;
     for (int j = 0; j < n; j++) {
-      sx = fma(A[(long)k * n + j], sp->s[j], sx);
-      sc = sc + A[(long)k * n + j];
+      const double v = A[(long)k * n + j];
+      /* ulaw 1 (MHRS bridge): ax = aa, the alive mass in states with exits */
+      sx = (ulaw == 1) ? sx + ((sp->s[j] > 0.0) ? v : 0.0) : fma(v, sp->s[j], sx);
+      sc = sc + v;
     }
     ax[k] = sx;
     ac[k] = sc;
@@ -308,15 +316,43 @@ static inline double orc_unif_R(const orc_sp *sp, double rinv, int c, int j) {
   return (c == j) ? fma(sp->S[c + c * n], rinv, 1.0) : sp->S[c + j * n] * rinv;
 }
 
+/* (k*, j*) from the Poisson weights and row k*'s end weights: e = 0 A s_j
+ * (fma), 1 A (add), 2 A 1[s_j > 0] (add) -- pht_unif.h unif_pick */
+static void orc_unif_pick(const orc_sp *sp, const double *A, const double *invk, const double *a, double lam,
+                          double W, int kend, int e, pht_stream *r, int *ks_out, int *js_out) {
+  const int n = sp->n;
+  const double target = pht_next_u(r) * W;
+  double w = 0x1p-1000, cum = 0.0;
+  int k = 0;
+  for (;;) {
+    cum = fma(w, a[k], cum);
+    if (cum >= target || k >= kend) break;
+    k++;
+    w = w * (lam * invk[k]);
+  }
+  const int ks = k;
+  const double *Ak = A + (long)ks * n;
+  const double t2 = pht_next_u(r) * a[ks];
+  double c2 = 0.0;
+  int js = n - 1;
+  for (int j = 0; j < n; j++) {
+    c2 = (e == 0) ? fma(Ak[j], sp->s[j], c2) : c2 + ((e == 1 || sp->s[j] > 0.0) ? Ak[j] : 0.0);
+    if (c2 >= t2) { js = j; break; }
+  }
+  *ks_out = ks;
+  *js_out = js;
+}
+
 static void orc_unif_obs(const orc_sp *sp, const double *T, double y, int cens, pht_stream *r, orc_obs *o,
-                         double zscale, int *neval) {
+                         double zscale, int *neval, int ulaw, int mhit) {
   const int n = sp->n;
   const int K = (int)T[2];
   const double mu = T[0], rinv = T[1];
   const double *invk = T + 4, *ax = invk + (K + 1), *ac = ax + (K + 1), *A = ac + (K + 1);
   orcD_obs_clear(o, n);
+  if (ulaw == 2) cens = 0; /* DCS treats censored observations as exact */
   const double lam = y * mu;
-  const double *a = cens ? ac : ax;
+  const double *a = cens ? ac : ax; /* ulaw 1: ax holds aa */
   int ok = (lam >= 0.0) && (lam <= ORC_UNIF_MAXLAM);
   int kend = 0;
   double W = 0.0;
@@ -337,23 +373,18 @@ static void orc_unif_obs(const orc_sp *sp, const double *T, double y, int cens, 
   }
   int b = 0, js = 0;
   if (ok) {
-    const double target = pht_next_u(r) * W;
-    double w = 0x1p-1000, cum = 0.0;
-    int k = 0;
-    for (;;) { /* pass 2: k* */
-      cum = fma(w, a[k], cum);
-      if (cum >= target || k >= kend) break;
-      k++;
-      w = w * (lam * invk[k]);
-    }
-    const int ks = k;
-    const double *Ak = A + (long)ks * n;
-    const double t2 = pht_next_u(r) * a[ks];
-    double c2 = 0.0;
-    js = n - 1;
-    for (int j = 0; j < n; j++) { /* j* */
-      c2 = cens ? c2 + Ak[j] : fma(Ak[j], sp->s[j], c2);
-      if (c2 >= t2) { js = j; break; }
+    const int e = cens ? 1 : (ulaw == 1 ? 2 : 0);
+    int ks;
+    orc_unif_pick(sp, A, invk, a, lam, W, kend, e, r, &ks, &js); /* pass 2: (k*, j*) */
+    if (ulaw == 1 && !cens) {
+      /* MHRS: mhit independence-MH steps, U < s[pre'] / s[pre]
+       * (src/Simulate_AbsCTMC_eq_Bladt_MHRS.c:79-82) */
+      for (int h = 0; h < mhit; h++) {
+        int kp, jp;
+        orc_unif_pick(sp, A, invk, a, lam, W, kend, e, r, &kp, &jp);
+        const double U = pht_next_u(r);
+        if (U < sp->s[jp] / sp->s[js]) { ks = kp; js = jp; }
+      }
     }
     b = js;
     double lt = 0.0, tend = y;
@@ -474,24 +505,27 @@ void orc_dev_sweep(const orc_sp *sp, int method, int mhit, const double *y, cons
   orc_obs o;
   int neval = 0, nbrent = 0;
   double *utab = NULL;
-  if (m == ORC_UNIF) {
+  /* the uniformisation kernels' path law: UNIF's own, or MHRS's / DCS's in
+   * bridge mode */
+  const int ulaw = (m == ORC_MHRS && orc_bridge_mhrs) ? 1 : ((m == ORC_DCS && orc_bridge_dcs) ? 2 : 0);
+  if (m == ORC_UNIF || ulaw) {
     double ymax = 0.0;
     for (long i = 0; i < l; i++) ymax = fmax(ymax, y[i]);
     const int K = orc_unif_K(sp, ymax);
     utab = (double *)malloc(sizeof(double) * orc_unif_tab_doubles(n, K));
-    orc_unif_table(sp, K, utab);
+    orc_unif_table(sp, K, utab, ulaw);
   }
   for (int k = 0; k < n; k++) { zq_tot[k] = 0; B_tot[k] = 0; }
   for (int k = 0; k < n * n; k++) N_tot[k] = 0;
   for (long i = 0; i < l; i++) {
     pht_stream r;
     pht_stream_init(&r, k0, k1, (uint32_t)(obs0 + i), 0u, sweep);
-    if (m == ORC_UNIF) orc_unif_obs(sp, utab, y[i], cens[i], &r, &o, zscale, &neval);
+    if (m == ORC_UNIF || ulaw) orc_unif_obs(sp, utab, y[i], cens[i], &r, &o, zscale, &neval, ulaw, mhit);
     else if (m == ORC_MHRS) orcD_obs_mhrs(sp, y[i], cens[i], mhit, &r, &o, zscale);
     else if (m == ORC_DCS) orcD_obs_dcs(sp, y[i], &r, &o, zscale, &nbrent);
     else if (cens[i]) orcD_obs_censored(sp, y[i], cens[i], &r, &o, zscale, &neval);
     else orcD_obs_ecs_exact(sp, y[i], &r, &o, zscale, &neval);
-    if (m != ORC_MHRS) o.ndraw = pht_stream_pos(&r);
+    if (m != ORC_MHRS || ulaw) o.ndraw = pht_stream_pos(&r);
     B_tot[o.B]++;
     for (int k = 0; k < n; k++) zq_tot[k] += o.zq[k];
     for (int k = 0; k < n * n; k++) N_tot[k] += o.N[k];

@@ -362,6 +362,10 @@ struct pht_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int n = 0, method = 0, mhit = 1;
+  /* the reference method asked for (dispatch_method), and the path law of the
+   * UNIF kernels when method is kMethodUNIF: 0 its own, 1 MHRS's / 2 DCS's
+   * law by uniformisation (PHT_MHRS=bridge, PHT_DCS=bridge; pht_unif.h) */
+  int rmethod = 0, ulaw = 0;
   long count = 0;
   long n_exact = 0;                      /* observations [0, n_exact) are exact (sorted first) */
   double *d_y = nullptr;
@@ -547,6 +551,7 @@ static int group_sweep(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   a.params = dp;
   a.n = c->n;
   a.mhit = c->mhit;
+  a.ulaw = c->ulaw;
   a.y = c->d_y;
   a.gid = c->d_gid;
   a.k0 = k0;
@@ -811,8 +816,21 @@ extern "C" pht_ctx *pht_ctx_create(int device, int n, int method, int mhit) {
   pht_ctx *c = new pht_ctx();
   c->device = device;
   c->n = n;
-  c->method = dispatch_method(method);
+  c->method = c->rmethod = dispatch_method(method);
   c->mhit = mhit;
+  /* bridge mode: MHRS or DCS path laws sampled exactly by the uniformisation
+   * kernels (pht_unif.h) instead of the rejection search / Hobolth's
+   * endpoint-conditioned sampler; same law, no eigensystem */
+  {
+    const char *em = getenv("PHT_MHRS"), *ed = getenv("PHT_DCS");
+    if (c->rmethod == kMethodMHRS && em && !strcmp(em, "bridge")) {
+      c->method = kMethodUNIF;
+      c->ulaw = 1;
+    } else if (c->rmethod == kMethodDCS && ed && !strcmp(ed, "bridge")) {
+      c->method = kMethodUNIF;
+      c->ulaw = 2;
+    }
+  }
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_params, make_layout(n).bytes()) != hipSuccess ||
       hipMalloc(&c->d_stats, sizeof(unsigned long long) * stats_len(n)) != hipSuccess ||
@@ -1058,6 +1076,7 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   a.params = c->d_params;
   a.n = c->n;
   a.mhit = c->mhit;
+  a.ulaw = c->ulaw;
   a.count = c->count;
   a.y = c->d_y;
   a.cens = c->d_cens;
@@ -1334,7 +1353,9 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
       say("CRITICAL ERROR: Unknown sampling method (code = %d)\n\n", method);
       continue;
     }
-    const int info = build_params(n, G.S.data(), G.s.data(), disp == kMethodMHRS ? kMethodMHRS : method, pb);
+    /* bridge contexts run the UNIF kernels: their block needs no eigensystem */
+    const int bm = ctxs[0]->ulaw ? kMethodUNIF : (disp == kMethodMHRS ? kMethodMHRS : method);
+    const int info = build_params(n, G.S.data(), G.s.data(), bm, pb);
     if (info < 0) return -1;
     for (pht_ctx *c : ctxs) {
       memcpy(c->h_params, pb.data(), pb.size());
@@ -1473,8 +1494,8 @@ extern "C" int pht_gibbs_run_chains(pht_ctx **ctxs, int nchains, const uint32_t 
   {
     bool one = nchains >= 2;
     for (int c = 0; c < nchains && one; c++)
-      one = ctxs[c]->method == ctxs[0]->method && ctxs[c]->device == ctxs[0]->device && ctxs[c]->n == ctxs[0]->n &&
-            !ctxs[c]->grp;
+      one = ctxs[c]->method == ctxs[0]->method && ctxs[c]->ulaw == ctxs[0]->ulaw &&
+            ctxs[c]->device == ctxs[0]->device && ctxs[c]->n == ctxs[0]->n && !ctxs[c]->grp;
     const char *ev = getenv("PHT_CHAINS_LAUNCH");
     if (ev && !strcmp(ev, "streams")) one = false;
     if (one) {
@@ -1556,12 +1577,12 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
     set_err("pht_gibbs_run_resident: need a context, it >= 1 and 1 <= m <= (kMaxN+1)^2");
     return -1;
   }
-  const int disp = dispatch_method(method);
-  if (disp == 0 || disp != c->method) {
+  if (dispatch_method(method) == 0 || dispatch_method(method) != c->rmethod) {
     set_err("pht_gibbs_run_resident: method %d needs a context created for that method (context %d)", method,
-            c->method);
+            c->rmethod);
     return -1;
   }
+  const int disp = c->method; /* the kernels that run (UNIF for a bridge context) */
   if (!(ldexp(c->ysum, zexp) < 0x1p62)) {
     set_err("zexp = %d overflows the fixed-point z sums (the shard's observed times total %g)", zexp, c->ysum);
     return -1;
@@ -1676,6 +1697,7 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
   a.params = c->d_params;
   a.n = n;
   a.mhit = c->mhit;
+  a.ulaw = c->ulaw;
   a.count = c->count;
   a.y = c->d_y;
   a.cens = c->d_cens;

@@ -61,6 +61,8 @@ struct SweepArgs {
   double *utab;
   int uK;
   double uymax;
+  int ulaw;                    /* the path law the UNIF kernels sample (pht_unif.h): 0 ECS/UNIF, 1 MHRS (with
+                                  mhit MH steps), 2 DCS (censored as exact) */
   /* debug per-observation outputs (DEBUG kernels only) */
   long long *dbg_zq;           /* [count*n] */
   int *dbg_N;                  /* [count*n*n] */

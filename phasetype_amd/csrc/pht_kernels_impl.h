@@ -1266,7 +1266,8 @@ __device__ __forceinline__ void unif_table_body(const SweepArgs &a) {
     double sx = 0.0, sc = 0.0;
     for (int j = 0; j < n; j++) {
       const double v = LDSA ? Al[(long)k * n + j] : A[(long)k * n + j];
-      sx = fma(v, d[L.s + j], sx);
+      /* ulaw 1 (MHRS bridge): ax = aa, the alive mass in states with exits */
+      sx = (a.ulaw == 1) ? sx + ((d[L.s + j] > 0.0) ? v : 0.0) : fma(v, d[L.s + j], sx);
       sc = sc + v;
     }
     ax[k] = sx;
@@ -1357,7 +1358,7 @@ __device__ __forceinline__ void unif_body(const SweepArgs &a, unsigned blk, unsi
       sk.dB = a.dbg_B + i;
       sk.dpre = a.dbg_pre + i;
     }
-    unif_obs<NT>(P, U, a.y[i], a.cens ? a.cens[i] : 0, ln, sk);
+    unif_obs<NT>(P, U, a.y[i], a.cens ? a.cens[i] : 0, ln, sk, a.ulaw, a.mhit);
     const uint32_t nd = pht_stream_pos(&ln.r);
     if (DEBUG) {
       a.dbg_flags[i] = ln.flags;

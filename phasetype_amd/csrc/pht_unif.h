@@ -48,7 +48,30 @@
  *     succPf (one word; an overrun takes the last candidate, flag 1), until
  *     absorption.
  * Draw order: U1 (k*), U2 (j*), [U time, U state] x k*, then the censored
- * continuation.  Flags: kFlagUnifCap (table end, lam cap, zero weights): the
+ * continuation.
+ *
+ * The same machinery samples the path laws of the reference's other two
+ * samplers exactly ("bridge" mode, SweepArgs::ulaw; PHT_MHRS=bridge,
+ * PHT_DCS=bridge):
+ *  - ulaw 1, MHRS (LJMA_MHsample_Bladt, src/Simulate_AbsCTMC_eq_Bladt_MHRS.c:
+ *    63-114): an attempt of LJMA_samplechain_Bladt is a forward path; the
+ *    first success is a draw of that path conditioned on success — exact:
+ *    alive at y in a state j with s_j > 0 (the re-draw loop :65-68), i.e.
+ *    (k*, j*) ~ Pois(k; lam) A_k[j] 1[s_j > 0] (the table's ax column then
+ *    holds aa_k = sum_j 1[s_j > 0] A_k[j], plain adds in increasing j, and
+ *    the j* scan adds 1[s_j > 0] A_k*[j]); censored: absorbed after y, i.e.
+ *    alive at y then forward, which is ulaw 0's censored law.  The reference
+ *    then runs mhit independence-MH steps (:70-101): proposal (k', j') the
+ *    same draw, accepted when U < s_j' / s_j*.  Here the current and every
+ *    proposal draw only (k*, j*) (two words each, plus the acceptance
+ *    uniform), the Poisson total W once; the accepted chain's path is then
+ *    bridged.  Draw order (exact): U1 U2 (current), [U1 U2 U] x mhit, the
+ *    bridge.  Same law as the rejection search, none of its attempts.
+ *  - ulaw 2, DCS (LJMA_MHsample_Hobolth2, src/Simulate_AbsCTMC_eq_
+ *    AslettHobolth_DCS.c:92-147): end state b ~ (pi e^{yS})_b s_b, then the
+ *    endpoint-conditioned path — ulaw 0's exact law; DCS treats censored
+ *    observations as exact (:132-133), so every observation runs ulaw 0's
+ *    exact mode.  Flags: kFlagUnifCap (table end, lam cap, zero weights): the
  * observation's path is then NOT a draw of the target law (a truncated
  * Poisson sum, or a placeholder path z(0) = y absorbed from state 0), so a
  * sweep with any such observation is an error (statistics word kXUnifCap;
@@ -99,12 +122,43 @@ __device__ __forceinline__ void unif_preds(const Par<NT> &P, double rinv, PHT_LD
   np[b] = q;
 }
 
+/* (k*, j*) from the Poisson weights w_k a_k (total W, the last row kend of
+ * pass 1) and row k*'s end weights: e = 0 A s_j (fma), 1 A (censored: add),
+ * 2 A 1[s_j > 0] (add) */
+template <int NT, class APtr>
+__device__ __forceinline__ void unif_pick(const Par<NT> &P, const UnifTab<APtr> &T, const PHT_LDS double *a,
+                                          double lam, double W, int kend, int e, Lane &ln, int &ks, int &js) {
+  const int n = P.n();
+  const double target = dev_u(ln.r) * W;
+  double w = 0x1p-1000, cum = 0.0;
+  int k = 0;
+  for (;;) {
+    cum = fma(w, a[k], cum);
+    if (cum >= target || k >= kend) break;
+    k++;
+    w = w * (lam * T.invk[k]);
+  }
+  ks = k;
+  const APtr Ak = T.A + (long)ks * n;
+  const double t2 = dev_u(ln.r) * a[ks];
+  double c2 = 0.0;
+  js = n - 1;
+  for (int j = 0; j < n; j++) {
+    c2 = (e == 0) ? fma(Ak[j], P.s(j), c2) : c2 + ((e == 1 || P.s(j) > 0.0) ? Ak[j] : 0.0);
+    if (c2 >= t2) {
+      js = j;
+      break;
+    }
+  }
+}
+
 template <int NT, class Sink, class APtr>
 __device__ __forceinline__ void unif_obs(const Par<NT> &P, const UnifTab<APtr> &T, double y, int cens, Lane &ln,
-                                         Sink &sk) {
+                                         Sink &sk, int ulaw = 0, int mhit = 0) {
   const int n = P.n();
+  if (ulaw == 2) cens = 0; /* DCS: censored observations are treated as exact */
   const double lam = y * T.mu;
-  const PHT_LDS double *a = cens ? T.ac : T.ax;
+  const PHT_LDS double *a = cens ? T.ac : T.ax; /* ulaw 1: ax holds aa */
   bool ok = (lam >= 0.0) && (lam <= kUnifMaxLam);
   int kend = 0;
   double W = 0.0;
@@ -128,25 +182,21 @@ __device__ __forceinline__ void unif_obs(const Par<NT> &P, const UnifTab<APtr> &
   }
   int b = 0, js = 0;
   if (ok) {
-    const double target = dev_u(ln.r) * W;
-    double w = 0x1p-1000, cum = 0.0;
-    int k = 0;
-    for (;;) {
-      cum = fma(w, a[k], cum);
-      if (cum >= target || k >= kend) break;
-      k++;
-      w = w * (lam * T.invk[k]);
-    }
-    const int ks = k;
-    const APtr Ak = T.A + (long)ks * n;
-    const double t2 = dev_u(ln.r) * a[ks];
-    double c2 = 0.0;
-    js = n - 1;
-    for (int j = 0; j < n; j++) {
-      c2 = cens ? c2 + Ak[j] : fma(Ak[j], P.s(j), c2);
-      if (c2 >= t2) {
-        js = j;
-        break;
+    const int e = cens ? 1 : (ulaw == 1 ? 2 : 0);
+    int ks;
+    unif_pick(P, T, a, lam, W, kend, e, ln, ks, js);
+    if (ulaw == 1 && !cens) {
+      /* MHRS: mhit independence-MH steps between draws of the same law,
+       * accepted when U < s[pre'] / s[pre] (src/Simulate_AbsCTMC_eq_Bladt_
+       * MHRS.c:79-82); only (k, j) of each draw is needed */
+      for (int h = 0; h < mhit; h++) {
+        int kp, jp;
+        unif_pick(P, T, a, lam, W, kend, e, ln, kp, jp);
+        const double U = dev_u(ln.r);
+        if (U < P.s(jp) / P.s(js)) {
+          ks = kp;
+          js = jp;
+        }
       }
     }
     /* backward bridge */

@@ -89,3 +89,27 @@ def test_reference_summaries_are_complete():
         assert int(s["sweeps"]) >= 0.85 * case[-1]
         for st in PO.STATS:
             assert np.all(s[st + "_se"] > 0) and np.all(np.isfinite(s[st]))
+
+
+@pytest.mark.parametrize("method,mhit,n,N,cf,grid", [(1, 1, 4, 30000, 0.0, True), (1, 5, 4, 30000, 0.0, True),
+                                                     (1, 1, 10, 20000, 0.3, False), (4, 1, 10, 20000, 0.3, False)])
+def test_bridge_device_spec_matches_reference_sweep(orc, method, mhit, n, N, cf, grid):
+    """The bridge modes' device specification (PHT_MHRS=bridge /
+    PHT_DCS=bridge: MHRS's / DCS's path law by uniformisation, pht_unif.h
+    ulaw 1 / 2) against the reference's own sampler ("ref" variant) on the
+    same (S, s, y), per cell within 5 se; the mhit = 1 grid case carries
+    MHRS's fresh-current-path bias, which the bridge must reproduce."""
+    from phasetype_amd.synth import bd_exit, simulate_ph
+
+    S, s = bd_exit(n)
+    y, cen = PO.grid_obs(N, 0.45, 0.55) if grid else simulate_ph(S, s, N, seed=3, censor_frac=cf)
+    orc.set_seed(11)
+    r = orc.ref_sweep(method, S, s, y, cen, mhit=mhit)
+    orc.set_bridge(mhrs=method == 1, dcs=method == 4)
+    try:
+        d = orc.dev_sweep(method, S, s, y, cen, mhit=mhit, key=(3, 4))
+    finally:
+        orc.set_bridge(False, False)
+    assert not d["flags"].any()
+    zs = PO.sweep_zscores(r["z"], r["N"], d["zq"] * 2.0 ** -d["zexp"], d["N"])
+    assert zs["z"].max() < PO.K_SIGMA and zs["N"].max() < PO.K_SIGMA, (zs["z"], zs["N"])
