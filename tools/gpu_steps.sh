@@ -13,6 +13,7 @@
 #   trace=<bench args>       rocprofv3 kernel trace of bench.py (tools/prof_trace.sh)
 #   pmc=<bench args>         rocprofv3 PMC passes + summary (tools/prof_pmc.sh, tools/pmc_summary.py)
 #   py=<script args>         python3 <script args> -> py_<k>.out
+#   env=NAME=VALUE           export for the following steps;  unenv=NAME  unset it
 # Outputs under gpurun_out/<tag>/; each GPU step has its own time limit and
 # the script stops at the first failure (no retries).
 set -o pipefail
@@ -64,6 +65,10 @@ for step in "$@"; do
       python3 tools/pmc_summary.py $R/gpurun_out/pmc_${TAG}_$k $O/pmc_${k}_summary.json $O/pmc_${k}_traffic.json \
         > $O/pmc_${k}_summary.out 2>&1 || { tail $O/pmc_${k}_summary.out; exit 1; }
       tail -25 $O/pmc_${k}_summary.out ;;
+    env)
+      export "$arg" ;;
+    unenv)
+      unset "$arg" ;;
     py)
       timeout -k 10 900 python3 -u $arg > $O/py_$k.out 2> $O/py_$k.err || { tail -20 $O/py_$k.err; exit 1; }
       tail -5 $O/py_$k.out ;;
