@@ -471,7 +471,9 @@ PHT_HD int pht_eig(int n, const double *S, double *evals, double *Q, double *Qin
  * chain).  Matrix products only: element-parallel, a handful of barriers per
  * round, where the QR iteration is a chain of dependent steps.  Stops when
  * max_{i != j} |B_ij| <= 64 eps max_i |B_ii|, or at its rounding floor (no
- * longer halving, below 1e-9 of the scale); returns PHT_EIG_NOCONV (the
+ * longer halving, below 1e-12 of the scale: the warm-started eigenvectors
+ * then reproduce S to ~1e-12 relative, against ~1e-15 from the QR/LAPACK
+ * path; a stall above that falls back to the QR); returns PHT_EIG_NOCONV (the
  * caller runs pht_eig) after PHT_EIG_REFINE_MAX rounds or when two diagonal
  * entries are closer than 2x the largest off-diagonal entry (the first-order
  * step needs |B_ki| well below |B_ii - B_kk|).
@@ -537,7 +539,7 @@ PHT_HD int pht_eig_refine(int n, const double *S, const double *Q0, const double
       gap = fmin(gap, rowg[i]);
       scale = fmax(scale, fabs(B[i + i * n]));
     }
-    if (off <= 64.0 * PHT_EIG_EPS * scale || (off >= 0.5 * prev && off <= 1e-9 * scale)) {
+    if (off <= 64.0 * PHT_EIG_EPS * scale || (off >= 0.5 * prev && off <= 1e-12 * scale)) {
       done = 1;
       break;
     }

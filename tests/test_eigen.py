@@ -115,6 +115,25 @@ def test_eig_refine_declines(orc):
         assert np.abs(Q2 @ np.diag(ev2) @ Qi2 - S2).max() < 1e-12
 
 
+@pytest.mark.parametrize("n", [3, 5, 8])
+def test_eig_refine_accuracy_bound(orc, n):
+    """a refinement accepted at its rounding floor (no longer
+    halving) must still be accurate: the accepted eigensystem diagonalises
+    the moved S to <= 1e-12 of its scale (the stall is accepted only below
+    that; above it the chain runs the full QR)."""
+    rng = np.random.default_rng(100 + n)
+    S, s = bd_exit(n)
+    rc, ev, Q, Qi = orc.eig(S)
+    for rel in (1e-4, 1e-3, 1e-2, 3e-2):
+        S2 = _moved(S, s, rel, rng)
+        rc2, ev2, Q2, Qi2 = orc.eig_refine(S2, Q, Qi)
+        if rc2 != 0:
+            continue
+        B = Qi2 @ S2 @ Q2
+        scale = np.abs(np.diag(B)).max()
+        assert np.abs(B - np.diag(np.diag(B))).max() <= 2e-12 * scale, (n, rel)
+
+
 @pytest.mark.parametrize("n,N", [(3, 2000), (5, 10000)])
 def test_resident_chain_warm_start_rarely_falls_back(orc, n, N):
     """Along the resident chain's own trajectory (oracle gibbs dev=2) the
