@@ -965,7 +965,11 @@ static long exact_rowk(const pht_ctx *c) {
    * the resident blocks) */
   const long L = kSpreadLanes;
   if (c->n_exact * 10 <= 6 * L) return 4096; /* 62.5k: 0.44 ms (1,024: 0.48; none: 0.56) */
-  if (c->n_exact <= 2 * L) return 1024;      /* 125k: 0.57 ms (4,096: 0.59; none: 0.62) */
+  /* the 8-GPU shards of cfg4 (125k each, r04 kernels; profiles/r04/rowk):
+   * max over the 8 real shards 0.487 ms at 2,048, 0.508 at 1,024, 0.498 at
+   * 4,096, 0.517 at 512 */
+  if (c->n_exact * 10 <= 12 * L) return 2048;
+  if (c->n_exact <= 2 * L) return 1024;      /* 250k (r02): 0.57 ms (4,096: 0.59; none: 0.62) */
   if (c->n_exact <= 5 * L) return 128;       /* cfg5's 350k exact: +5 % */
   return 0;                                  /* cfg4's 10^6: rows cost the one-lane range more (K = 64: +1 %) */
 }
