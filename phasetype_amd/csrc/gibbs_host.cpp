@@ -385,6 +385,11 @@ struct pht_ctx {
   double *d_utab = nullptr;              /* UNIF per-sweep table (pht_unif.h) */
   long utab_cap = 0;                     /* its capacity in doubles */
   int *d_dcsb = nullptr;                 /* DCS: per-position end states (dcs_end_kernel) */
+  /* ECS hand-off records (strong-scaling regime, SweepArgs::hand) */
+  EcsCont *d_cbuf = nullptr;
+  unsigned *d_cready = nullptr, *d_cq = nullptr;
+  long cont_cap = 0;
+  unsigned cepoch = 0;
   /* debug buffers */
   long long *d_zq = nullptr;
   int *d_N = nullptr, *d_B = nullptr, *d_pre = nullptr, *d_flags = nullptr;
@@ -623,6 +628,12 @@ static void ctx_free_obs(pht_ctx *c) {
   c->utab_cap = 0;
   if (c->d_dcsb) (void)hipFree(c->d_dcsb);
   c->d_dcsb = nullptr;
+  if (c->d_cbuf) (void)hipFree(c->d_cbuf);
+  if (c->d_cready) (void)hipFree(c->d_cready);
+  if (c->d_cq) (void)hipFree(c->d_cq);
+  c->d_cbuf = nullptr;
+  c->d_cready = c->d_cq = nullptr;
+  c->cont_cap = 0;
   c->d_y = nullptr; c->d_cens = nullptr; c->d_gid = nullptr;
   c->d_mbest = c->d_mq0 = c->d_mq1 = nullptr;
   c->d_mcnt = nullptr;
@@ -943,6 +954,15 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
     const bool pre = e ? atoi(e) != 0 : count >= kDcsPrepassMin;
     if (c->method == kMethodDCS && pre) HIPCHK(hipMalloc(&c->d_dcsb, sizeof(int) * count));
   }
+  /* ECS hand-off records: one per exact observation at most (each is handed
+   * off at most once), where the policy can turn it on */
+  if (c->method == kMethodECS && c->n_exact > 0 && (c->n_exact <= 2 * kSpreadLanes || getenv("PHT_HAND"))) {
+    HIPCHK(hipMalloc(&c->d_cbuf, sizeof(EcsCont) * c->n_exact));
+    HIPCHK(hipMalloc(&c->d_cready, sizeof(unsigned) * c->n_exact));
+    HIPCHK(hipMalloc(&c->d_cq, sizeof(unsigned) * kContQ));
+    HIPCHK(hipMemset(c->d_cready, 0, sizeof(unsigned) * c->n_exact));
+    c->cont_cap = c->n_exact;
+  }
   return 0;
 }
 
@@ -972,6 +992,15 @@ static long exact_rowk(const pht_ctx *c) {
   if (c->n_exact <= 2 * L) return 1024;      /* 250k (r02): 0.57 ms (4,096: 0.59; none: 0.62) */
   if (c->n_exact <= 5 * L) return 128;       /* cfg5's 350k exact: +5 % */
   return 0;                                  /* cfg4's 10^6: rows cost the one-lane range more (K = 64: +1 %) */
+}
+
+/* ECS hand-off threshold (SweepArgs::hand): with rows in the launch, a
+ * one-lane path still running after this many jumps continues on a row.
+ * PHT_HAND=k forces it (0 = off) */
+static int exact_hand(const pht_ctx *c) {
+  if (!c->d_cbuf) return 0;
+  if (const char *e = getenv("PHT_HAND")) return std::max(0, atoi(e));
+  return 0;
 }
 
 /* UNIF: size (and grow) the context's table for this sweep's parameters
@@ -1026,6 +1055,17 @@ static int ctx_launch(pht_ctx *c, const SweepArgs &a, bool debug) {
     ae.occ = exact_occ(c);
     ae.rowk = exact_rowk(c);
     ae.rowprio = getenv("PHT_ROWPRIO") ? atoi(getenv("PHT_ROWPRIO")) : 3;
+    ae.hand = ae.rowk > 0 ? exact_hand(c) : 0;
+    if (ae.hand > 0) {
+      ae.cbuf = c->d_cbuf;
+      ae.cready = c->d_cready;
+      ae.cq = c->d_cq;
+      ae.ccap = c->cont_cap;
+      if (++c->cepoch == 0) c->cepoch = 1; /* a record is current when its flag holds this launch's epoch */
+      ae.cepoch = c->cepoch;
+      ae.contblk = getenv("PHT_HANDBLK") ? atoi(getenv("PHT_HANDBLK")) : 32;
+      HIPCHK(hipMemsetAsync(c->d_cq, 0, sizeof(unsigned) * kContQ, c->stream));
+    }
     /* lane-major first claims when the shard is within ~2 observations per
      * lane (the longest paths, one per wavefront; tools/latency.py:
      * -10 % at 31k-125k per GPU); PHT_SPREAD=0|1 forces it */
