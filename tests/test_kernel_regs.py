@@ -25,7 +25,7 @@ def regs(lib):
 
 
 @pytest.mark.parametrize("nt", [3, 5, 10, 15])
-@pytest.mark.parametrize("kind", ["ecs_exact_kernelILi{nt}ELb0ELb0E", "ecs_exact_kernelILi{nt}ELb0ELb1E",
+@pytest.mark.parametrize("kind", ["ecs_exact_kernelILi{nt}ELb0ELb0ELb0E", "ecs_exact_kernelILi{nt}ELb0ELb1ELb0E",
                                   "ecs_chains_kernelILi{nt}EE"])
 def test_ecs_two_waves_no_spill(regs, nt, kind):
     key = kind.format(nt=nt)
@@ -34,6 +34,18 @@ def test_ecs_two_waves_no_spill(regs, nt, kind):
     (name, d), = hits.items()
     assert d["waves_per_simd"] >= 2, (name, d)
     assert d["vgpr_spill"] == 0, (name, d)
+
+
+@pytest.mark.parametrize("nt", [3, 5, 10, 15])
+def test_ecs_handoff_instantiation(regs, nt):
+    """The hand-off kernel (its own instantiation, launched only in the
+    strong-scaling regime, PHT_HAND) keeps two waves per SIMD; its spills are
+    bounded (the kernels without hand-off above must have none)."""
+    key = f"ecs_exact_kernelILi{nt}ELb0ELb1ELb1E"
+    hits = {k: v for k, v in regs.items() if key in k}
+    assert len(hits) == 1, (key, list(hits))
+    (name, d), = hits.items()
+    assert d["waves_per_simd"] >= 2 and d["vgpr_spill"] <= 128, (name, d)
 
 
 def test_mhrs_search_occupancy(regs):
@@ -49,7 +61,7 @@ def test_ecs_debug_instantiations(regs, nt):
     outputs; the parity tests run them, nothing times them): they may spill
     a few VGPRs (n = 15: 6, n = 20: 18 at r01, 51 at r03 after the absorb
     test moved to U den < exp(.)) but must not blow up."""
-    key = f"ecs_exact_kernelILi{nt}ELb1ELb{int(0 < nt <= 16)}E"
+    key = f"ecs_exact_kernelILi{nt}ELb1ELb{int(0 < nt <= 16)}ELb0E"
     hits = {k: v for k, v in regs.items() if key in k}
     assert len(hits) == 1, (key, list(hits))
     (name, d), = hits.items()
