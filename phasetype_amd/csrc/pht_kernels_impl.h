@@ -697,7 +697,7 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
             EcsCont *c = a.cbuf + idx;
             /* (the next absorb test's denominator is not carried: the row
              * recomputes it, the same pht_dot16 of the same vectors) */
-            c->pos = pos;
+            if (DEBUG) c->pos = pos; /* (only the per-observation outputs need it: no live range otherwise) */
             c->yt = st.yt;
             c->j = st.j;
             c->njump = st.njump;
@@ -944,7 +944,7 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
             /* the path's state at its jump boundary: its absorb test is next
              * (the denominator is recomputed: the same pht_dot16) */
             const EcsCont *c = a.cbuf + cidx;
-            pos = c->pos;
+            if (DEBUG) pos = c->pos;
             ln.r = c->r;
             ln.flags = c->flags;
             ln.neval = c->neval;
