@@ -708,6 +708,11 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
 #pragma unroll
             for (int i = 0; i < PHT_VEC(NT); i++)
               if (i < n) c->E0[i] = st.E0[i];
+#ifdef PHT_TRACE_HAND
+            if (idx < 3)
+              printf("P idx=%u pos=%ld yt=%.17g j=%d nj=%d blk=%u na=%d nb=%d E0=%.17g fl=%d\n", idx, pos, st.yt, st.j,
+                     st.njump, ln.r.blk, ln.r.na, ln.r.nb, st.E0[0], ln.flags);
+#endif
             __threadfence();
             __hip_atomic_store(&a.cready[idx], a.cepoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             have = false;
@@ -922,13 +927,18 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
           /* continuation rows (hand-off): claim the next record, then poll
            * for it once per round, never blocking the wave's other rows;
            * leave when every one-lane wave is done and no record is left */
-          if (!rowq[rq][0]) {
-            if (id.lead) {
+          /* rowq is read and written by the row's lead lane only and
+           * broadcast with __shfl: a plain LDS read by the other lanes would
+           * race with the lead's store (the compiler may keep an old value) */
+          unsigned cidx = 0;
+          if (id.lead) {
+            if (!rowq[rq][0]) {
               rowq[rq][1] = atomicAdd(&a.cq[1], 1u);
               rowq[rq][0] = 1u;
             }
+            cidx = rowq[rq][1];
           }
-          const unsigned cidx = rowq[rq][1];
+          cidx = (unsigned)__shfl((int)cidx, 0, kRowW);
           const unsigned nwaves_main = (unsigned)a.nmain * (kBlock / 64);
           unsigned e = 0, dn = 0, al = 0;
           const bool inb = cidx < (unsigned long)a.ccap;
@@ -942,7 +952,10 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
           al = (unsigned)__shfl((int)al, 0, kRowW);
           if (inb && e == a.cepoch) {
             /* the path's state at its jump boundary: its absorb test is next
-             * (the denominator is recomputed: the same pht_dot16) */
+             * (the denominator is recomputed: the same pht_dot16).  Every lane
+             * orders its reads of the record after the lead's observation of
+             * the flag (agent-scope acquire: invalidates this CU's L1) */
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             const EcsCont *c = a.cbuf + cidx;
             if (DEBUG) pos = c->pos;
             ln.r = c->r;
@@ -966,6 +979,11 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
             }
             if (id.lead) rowq[rq][0] = 0u;
             have = true;
+#ifdef PHT_TRACE_HAND
+            if (cidx < 3 && id.rl < 2)
+              printf("C cidx=%u rl=%d pos=%ld yt=%.17g j=%d nj=%d blk=%u na=%d nb=%d E0v0=%.17g fl=%d\n", cidx, id.rl, pos,
+                     st.yt, st.j, st.njump, ln.r.blk, ln.r.na, ln.r.nb, st.E0.v[0], ln.flags);
+#endif
           } else if (!inb || (dn >= nwaves_main && cidx >= al)) {
             done = true;
             break;
