@@ -1063,7 +1063,7 @@ static int ctx_launch(pht_ctx *c, const SweepArgs &a, bool debug) {
       ae.ccap = c->cont_cap;
       if (++c->cepoch == 0) c->cepoch = 1; /* a record is current when its flag holds this launch's epoch */
       ae.cepoch = c->cepoch;
-      ae.contblk = getenv("PHT_HANDBLK") ? atoi(getenv("PHT_HANDBLK")) : 32;
+      ae.contblk = getenv("PHT_HANDBLK") ? atoi(getenv("PHT_HANDBLK")) : 128;
       HIPCHK(hipMemsetAsync(c->d_cq, 0, sizeof(unsigned) * kContQ, c->stream));
     }
     /* lane-major first claims when the shard is within ~2 observations per

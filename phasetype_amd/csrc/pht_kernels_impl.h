@@ -1099,21 +1099,22 @@ ecs_exact_kernel(SweepArgs a) {
       ecs_row_body<NT, DEBUG>(a, blockIdx.x, (unsigned)a.rowblk);
       return;
     }
-    if constexpr (HAND) {
-      /* hand-off (its own instantiation, so the kernels without it keep
-       * their register allocation): blocks [rowblk, rowblk + contblk)
-       * continue, on rows, the paths the one-lane blocks hand off */
-      if (__builtin_expect(blockIdx.x < (unsigned)(a.rowblk + a.contblk), 0)) {
-        ecs_row_body<NT, DEBUG, true>(a, blockIdx.x - (unsigned)a.rowblk, (unsigned)a.contblk);
-        return;
-      }
-      ecs_exact_body<NT, DEBUG, true>(a, blockIdx.x - (unsigned)(a.rowblk + a.contblk), (unsigned)a.nmain);
-    } else {
-      ecs_exact_body<NT, DEBUG>(a, blockIdx.x - (unsigned)a.rowblk, (unsigned)a.nmain);
-    }
+    /* HAND (its own instantiation, so the kernels without it keep their
+     * register allocation): the one-lane blocks hand off their long paths;
+     * ecs_cont_kernel continues them after this launch */
+    ecs_exact_body<NT, DEBUG, HAND>(a, blockIdx.x - (unsigned)a.rowblk, (unsigned)a.nmain);
   } else {
     ecs_exact_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
   }
+}
+
+/* the hand-off's continuation launch: rows take the records the one-lane
+ * blocks of the launch before wrote (all complete), until none is left */
+template <int NT, bool DEBUG>
+__global__ void __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu(DEBUG ? 1 : ecs_waves<NT, true>())))
+ecs_cont_kernel(SweepArgs a) {
+  ecs_row_body<NT, DEBUG, true>(a, blockIdx.x, gridDim.x);
 }
 
 /*
@@ -1166,21 +1167,22 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
   b.rowk = std::max(0L, rk);
   b.rowblk = (int)((b.rowk + (kBlock / kRowW) - 1) / (kBlock / kRowW));
   if (b.rowblk == 0 || !rows) b.hand = 0; /* hand-off needs rows to take the paths */
-  /* continuation blocks (hand-off), taken from the one-lane blocks' slots */
-  b.contblk = (b.hand > 0) ? (int)std::max(1L, std::min((long)a.contblk, slots - b.rowblk - 1)) : 0;
-  if (b.hand > 0 && slots - b.rowblk - b.contblk < 1) b.hand = 0, b.contblk = 0;
+  /* continuation launch (hand-off): its blocks, after the main launch */
+  b.contblk = (b.hand > 0) ? (int)std::max(1L, std::min((long)a.contblk, slots)) : 0;
   b.begin = a.begin + b.rowk;
   b.count = a.count - b.rowk;
   const long want = (b.count + kBlock - 1) / kBlock;
-  long grid = slots - b.rowblk - b.contblk;
+  long grid = slots - b.rowblk;
   if (grid > want) grid = want;
   if (grid < 0) grid = 0;
   b.nmain = (int)grid;
   if (grid + b.rowblk < 1) return hipSuccess;
-  if (rows && b.hand > 0)
-    hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG, row_ok<NT>(), true>), dim3((unsigned)(grid + b.rowblk + b.contblk)),
+  if (rows && b.hand > 0) {
+    hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG, row_ok<NT>(), true>), dim3((unsigned)(grid + b.rowblk)),
                        dim3(kBlock), sm, st, b);
-  else if (rows)
+    if constexpr (row_ok<NT>())
+      hipLaunchKernelGGL((ecs_cont_kernel<NT, DEBUG>), dim3((unsigned)b.contblk), dim3(kBlock), sm, st, b);
+  } else if (rows)
     hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG, row_ok<NT>()>), dim3((unsigned)(grid + b.rowblk)), dim3(kBlock), sm,
                        st, b);
   else
