@@ -1228,10 +1228,14 @@ static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
         e != hipSuccess)
       return e;
     if (hipMemsetAsync(a.mbest, 0xff, sizeof(uint32_t) * tasks, st) != hipSuccess) return hipErrorUnknown;
-    const dim3 g((unsigned)(cus * occc)), gc(256);
+    /* compaction grids: after round 0 every task is scanned, one per thread
+     * (with 256 blocks each thread walked ~30 tasks serially: 0.11 ms of a
+     * 1.5 ms cfg4 sweep, profiles/r04/mhrs_ab/); the later queues are short */
+    const dim3 g((unsigned)(cus * occc)), gc(256),
+        gc0((unsigned)std::min(std::max((tasks + kBlock - 1) / kBlock, 1L), 65535L));
     unsigned *c = a.mcnt;
     hipLaunchKernelGGL((mhrs_search<NT, 1, kMhrsK0>), g, dim3(kBlock), smc, st, a, 0u, nullptr, nullptr);
-    hipLaunchKernelGGL((mhrs_compact<NT>), gc, dim3(kBlock), 0, st, a, nullptr, nullptr, a.mq0, c + 0);
+    hipLaunchKernelGGL((mhrs_compact<NT>), gc0, dim3(kBlock), 0, st, a, nullptr, nullptr, a.mq0, c + 0);
     constexpr MhrsRound R1 = kMhrsRounds[0], R2 = kMhrsRounds[1], R3 = kMhrsRounds[2], R4 = kMhrsRounds[3],
                         R5 = kMhrsRounds[4];
     hipLaunchKernelGGL((mhrs_search<NT, R1.W, R1.K>), g, dim3(kBlock), smc, st, a, R1.A0, a.mq0, c + 0);
@@ -1710,10 +1714,13 @@ static hipError_t launch_chains(const SweepArgs *h, const SweepArgs *d, int K, i
     const dim3 g((unsigned)(nb * K));
     const long nbc = std::max(1L, 256L / K);
     const dim3 gc((unsigned)(nbc * K));
+    /* the first compaction scans every task: one per thread (launch_mhrs_search) */
+    const long nbc0 = std::max(1L, std::min(65535L / K, (maxt + kBlock - 1) / kBlock));
+    const dim3 gc0((unsigned)(nbc0 * K));
     constexpr MhrsRound R1 = kMhrsRounds[0], R2 = kMhrsRounds[1], R3 = kMhrsRounds[2], R4 = kMhrsRounds[3],
                         R5 = kMhrsRounds[4];
     hipLaunchKernelGGL((mhrs_search_chains<NT, 1, kMhrsK0>), g, dim3(kBlock), smc, st, d, K, (unsigned)nb, 0, 0u);
-    hipLaunchKernelGGL((mhrs_compact_chains<NT>), gc, dim3(kBlock), 0, st, d, K, (unsigned)nbc, 0);
+    hipLaunchKernelGGL((mhrs_compact_chains<NT>), gc0, dim3(kBlock), 0, st, d, K, (unsigned)nbc0, 0);
     hipLaunchKernelGGL((mhrs_search_chains<NT, R1.W, R1.K>), g, dim3(kBlock), smc, st, d, K, (unsigned)nb, 1, R1.A0);
     hipLaunchKernelGGL((mhrs_compact_chains<NT>), gc, dim3(kBlock), 0, st, d, K, (unsigned)nbc, 1);
     hipLaunchKernelGGL((mhrs_search_chains<NT, R2.W, R2.K>), g, dim3(kBlock), smc, st, d, K, (unsigned)nb, 2, R2.A0);
