@@ -287,10 +287,49 @@ __global__ void __launch_bounds__(kBlock) mhrs_search(SweepArgs a, uint32_t A0, 
 /* tasks of qin still unresolved -> qout */
 __device__ __forceinline__ void mhrs_compact_body(const SweepArgs &a, const uint32_t *qin, const unsigned *cin,
                                                   uint32_t *qout, unsigned *cout, unsigned blk, unsigned nblk) {
+  /* ONE counter atomic per block: block b owns a contiguous range of the
+   * queue, counts its unresolved tasks, reserves that many slots, then
+   * writes them (wavefront ballots, LDS offsets).  A counter atomic per task
+   * or per wavefront (device scope, one address) made the first compaction
+   * ~0.1 ms at cfg4 (profiles/r04/mhrs_ab/).  The queue's order does not
+   * matter: attempt streams are per (task, attempt). */
+  __shared__ unsigned wsum[kBlock / 64], sbase;
   const long cnt = qin ? (long)(*cin) : a.count * (1 + a.mhit);
-  for (long q = (long)blk * kBlock + threadIdx.x; q < cnt; q += (long)nblk * kBlock) {
-    const uint32_t task = qin ? qin[q] : (uint32_t)q;
-    if (a.mbest[task] == kMhrsUnresolved) qout[atomicAdd(cout, 1u)] = task;
+  const long per = ((cnt + nblk - 1) / nblk + kBlock - 1) / kBlock * kBlock;
+  const long lo = (long)blk * per, hi = (lo + per < cnt) ? lo + per : cnt;
+  if (lo >= hi) return; /* (uniform per block) */
+  const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  auto unres = [&](long q, uint32_t &task) {
+    task = qin ? qin[q] : (uint32_t)q;
+    return a.mbest[task] == kMhrsUnresolved;
+  };
+  unsigned mine = 0;
+  for (long q = lo + threadIdx.x; q < hi; q += kBlock) {
+    uint32_t task;
+    mine += unres(q, task) ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o);
+  if (lane == 0) wsum[wv] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned tot = 0;
+    for (int w = 0; w < kBlock / 64; w++) tot += wsum[w];
+    sbase = tot ? atomicAdd(cout, tot) : 0u;
+  }
+  __syncthreads();
+  unsigned base = sbase;
+  for (long q0 = lo; q0 < hi; q0 += kBlock) {
+    const long q = q0 + threadIdx.x;
+    uint32_t task = 0;
+    const bool un = (q < hi) && unres(q, task);
+    const unsigned long long m = __ballot(un);
+    __syncthreads(); /* (the previous step's wsum reads are done) */
+    if (lane == 0) wsum[wv] = (unsigned)__popcll(m);
+    __syncthreads();
+    unsigned off = base;
+    for (unsigned w = 0; w < wv; w++) off += wsum[w];
+    if (un) qout[off + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] = task;
+    for (int w = 0; w < kBlock / 64; w++) base += wsum[w];
   }
 }
 /* (templated only to keep one copy per pht_kernels_nt.hip unit) */
@@ -1228,11 +1267,10 @@ static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
         e != hipSuccess)
       return e;
     if (hipMemsetAsync(a.mbest, 0xff, sizeof(uint32_t) * tasks, st) != hipSuccess) return hipErrorUnknown;
-    /* compaction grids: after round 0 every task is scanned, one per thread
-     * (with 256 blocks each thread walked ~30 tasks serially: 0.11 ms of a
-     * 1.5 ms cfg4 sweep, profiles/r04/mhrs_ab/); the later queues are short */
+    /* compaction grids: after round 0 every task is scanned (~4096 per
+     * block); the later queues are short */
     const dim3 g((unsigned)(cus * occc)), gc(256),
-        gc0((unsigned)std::min(std::max((tasks + kBlock - 1) / kBlock, 1L), 65535L));
+        gc0((unsigned)std::min(std::max((tasks + 4095) / 4096, 1L), 1024L));
     unsigned *c = a.mcnt;
     hipLaunchKernelGGL((mhrs_search<NT, 1, kMhrsK0>), g, dim3(kBlock), smc, st, a, 0u, nullptr, nullptr);
     hipLaunchKernelGGL((mhrs_compact<NT>), gc0, dim3(kBlock), 0, st, a, nullptr, nullptr, a.mq0, c + 0);
@@ -1714,8 +1752,8 @@ static hipError_t launch_chains(const SweepArgs *h, const SweepArgs *d, int K, i
     const dim3 g((unsigned)(nb * K));
     const long nbc = std::max(1L, 256L / K);
     const dim3 gc((unsigned)(nbc * K));
-    /* the first compaction scans every task: one per thread (launch_mhrs_search) */
-    const long nbc0 = std::max(1L, std::min(65535L / K, (maxt + kBlock - 1) / kBlock));
+    /* the first compaction scans every task (launch_mhrs_search) */
+    const long nbc0 = std::max(1L, std::min(std::max(1024L / K, 1L), (maxt + 4095) / 4096));
     const dim3 gc0((unsigned)(nbc0 * K));
     constexpr MhrsRound R1 = kMhrsRounds[0], R2 = kMhrsRounds[1], R3 = kMhrsRounds[2], R4 = kMhrsRounds[3],
                         R5 = kMhrsRounds[4];
