@@ -207,6 +207,13 @@ class OracleLib:
         device spec's default safeguarded Halley iteration (off)."""
         self.lib.orc_set_dcs_brent(1 if on else 0)
 
+    def halley_hist(self) -> np.ndarray:
+        """evaluations per DCS jump of the dev variant's Halley root since the
+        last call (bins 0..63, the last = 63 or more); clears the counts"""
+        h = np.zeros(64, np.int64)
+        self.lib.orc_halley_hist_take(h.ctypes.data_as(C.c_void_p))
+        return h
+
     def set_bridge(self, mhrs: bool = False, dcs: bool = False) -> None:
         """dev variant's bridge modes (PHT_MHRS=bridge / PHT_DCS=bridge on the
         device): MHRS's / DCS's path law sampled exactly by the

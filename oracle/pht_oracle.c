@@ -37,6 +37,15 @@ double orc_norm_rand(void) { return pht_rs_norm_rand(&g_rs); }
 /* dev variant's DCS jump-time root finder: 0 = hob_halley (the device
  * spec's default), 1 = Find02 (PHT_DCS_ROOT=brent on the device) */
 static int orc_dcs_brent = 0;
+/* evaluations per DCS jump of the dev variant's Halley root (histogram,
+ * last bin = 63 or more); read and cleared by orc_halley_hist_take */
+static long orc_halley_hist[64];
+void orc_halley_hist_take(long *out) {
+  for (int k = 0; k < 64; k++) {
+    if (out) out[k] = orc_halley_hist[k];
+    orc_halley_hist[k] = 0;
+  }
+}
 void orc_set_dcs_brent(int on) { orc_dcs_brent = on; }
 
 /* dev variant's bridge modes (PHT_MHRS=bridge / PHT_DCS=bridge on the

@@ -997,20 +997,22 @@ static double ORC_FN(hob_halley)(const ORC_FN(hob_ctx) *c, double es, int *nev) 
     double tmp = 0.0, asum = 0.0, dtmp = 0.0, d2 = 0.0;
     for (int i = 0; i < n; i++) {
       const double Ei = c->E[i], ev = sp->evals[i];
-      double ei, Ji, dl;
+      double ei, Ji, dl, Jm;
       if (fabs((ev - Sll) / Sll) < 1e-13) {
         ei = Ei;
         Ji = xb * Ei;
         dl = 0.0;
+        Jm = fabs(Ji);
       } else {
         ei = ORC_EXP_NEG(c1 * ev + c0);
         Ji = (Ei - ei) * (1.0 / (ev - Sll));
         dl = Sll - ev;
+        Jm = (Ei + ei) * fabs(1.0 / (ev - Sll)); /* |J_i| before E_i - e_i cancels */
       }
       const double q = sp->Q[c->j + i * n], qb = c->Qb[i];
       const double qJ = q * Ji, qe = q * ei;
       tmp = fma(qJ, qb, tmp);
-      asum = fma(fabs(qJ), fabs(qb), asum);
+      asum = fma(fabs(q) * Jm, fabs(qb), asum);
       dtmp = fma(qe, qb, dtmp);
       d2 = fma(qe * dl, qb, d2);
     }
@@ -1152,6 +1154,7 @@ static void ORC_FN(obs_dcs)(const orc_sp *sp, double y, ORC_FN(rng) *rng, orc_ob
       int nev = 0;
       jtime = ORC_FN(hob_halley)(&hc, ORC_EXP_NEG(Sjj * x), &nev);
       if (nbrent) *nbrent += nev;
+      orc_halley_hist[nev < 63 ? nev : 63]++; /* diagnostics: tools/dcs_halley_hist.py */
     } else
 #endif
     {

@@ -118,12 +118,17 @@ __device__ __forceinline__ void brent_tail(BrentSt &s, double fb) {
  * the sign bracket [lo, hi] (F(0) = -u < 0 < 1 - u = F(X)); the Halley point
  * x - 2 F F' / (2 F'^2 - F F'') is replaced by the bracket's midpoint when it
  * is not strictly inside.  Stops when |F| is within 16 ulps of the
- * magnitudes it is summed from (16 eps (coef sum_i |Q_ji J_i Qb_i| + u):
- * below that F's own rounding decides; the Halley point is returned if it is
- * in the bracket), when a step moves x by at most 2 eps |x| (Find02's
- * tol_act at Tol = 0), or after 1000 evaluations (Find02's Maxit).  The
- * root agrees with Find02's to the evaluation's rounding (~1e-12 relative);
- * ~3.8 evaluations per jump at n = 3..20 (p90 4) where Find02 takes ~11.
+ * magnitudes it is computed from, 16 eps (coef sum_i |Q_ji| |J_i| |Qb_i| +
+ * u) with |J_i| taken BEFORE E_i - e_i cancels ((E_i + e_i) / |lambda_i -
+ * S_jj|): below that F's own rounding decides (the Halley point is returned
+ * if it is in the bracket); when a step moves x by at most 2 eps |x|
+ * (Find02's tol_act at Tol = 0); or after 1000 evaluations (Find02's Maxit).
+ * The root agrees with Find02's to the evaluation's rounding (~1e-10
+ * relative at worst, the same as before r04's bound).  r04: the bound used
+ * |J_i| after the cancellation, which is far below F's actual rounding when
+ * x is small; ~3 % of jumps then bisected for 6-30 evaluations at the noise
+ * floor, and a wavefront's round waits for its slowest lane (E[max of 64]
+ * 9.9 -> 5.5 evaluations, mean 3.8 -> 3.5).
  */
 /* a lane's e^{lambda_i (y - t)}: registers for small n, lane-interleaved
  * LDS rows from n = 10, where registers spilled
@@ -168,20 +173,22 @@ __device__ __forceinline__ double hob_halley(const Par<NT> &P, const DcsE<NT> &E
 #pragma unroll
     for (int i = 0; i < n; i++) {
       const double Ei = E.get(i), ev = P.evals(i);
-      double ei, Ji, dl;
+      double ei, Ji, dl, Jm;
       if ((near >> i) & 1u) {
         ei = Ei;
         Ji = xb * Ei;
         dl = 0.0;
+        Jm = fabs(Ji);
       } else {
         ei = pht_exp_neg(c1 * ev + c0);
         Ji = (Ei - ei) * rv[i];
         dl = Sjj - ev;
+        Jm = (Ei + ei) * fabs(rv[i]); /* |J_i| before E_i - e_i cancels */
       }
       const double q = P.Q(jn, i), qb = P.Qinv(i, b);
       const double qJ = q * Ji, qe = q * ei;
       tmp = fma(qJ, qb, tmp);
-      asum = fma(fabs(qJ), fabs(qb), asum);
+      asum = fma(fabs(q) * Jm, fabs(qb), asum);
       dtmp = fma(qe, qb, dtmp);
       d2 = fma(qe * dl, qb, d2);
       PHT_DCS_CHUNK(i);
