@@ -13,6 +13,7 @@
 #   trace=<bench args>       rocprofv3 kernel trace of bench.py (tools/prof_trace.sh)
 #   pmc=<bench args>         rocprofv3 PMC passes + summary (tools/prof_pmc.sh, tools/pmc_summary.py)
 #   py=<script args>         python3 <script args> -> py_<k>.out
+#   configs                  tools/gpu_configs.sh: bench.py at every BASELINE config -> <tag>_cfgs/
 #   env=NAME=VALUE           export for the following steps;  unenv=NAME  unset it
 # Outputs under gpurun_out/<tag>/; each GPU step has its own time limit and
 # the script stops at the first failure (no retries).
@@ -69,6 +70,9 @@ for step in "$@"; do
       export "$arg" ;;
     unenv)
       unset "$arg" ;;
+    configs)
+      bash tools/gpu_configs.sh ${TAG}_cfgs || { echo "configs failed"; exit 1; }
+      cp $R/gpurun_out/${TAG}_cfgs/*.json $O/ 2>/dev/null ;;
     py)
       timeout -k 10 900 python3 -u $arg > $O/py_$k.out 2> $O/py_$k.err || { tail -20 $O/py_$k.err; exit 1; }
       tail -5 $O/py_$k.out ;;
