@@ -1022,6 +1022,14 @@ static double ORC_FN(hob_halley)(const ORC_FN(hob_ctx) *c, double es, int *nev) 
     if (F < 0.0) lo = xb;
     else hi = xb;
     double nx = xb - (2.0 * F * D) / (2.0 * D * D - F * D2);
+    if (it == 0) { /* the first step in log-survival space (pht_dcs_round.h) */
+      const double S = (1.0 - c->u) - F;
+      if (S > 0.0) {
+        const double q = D / S, G = ORC_LOG(S / (1.0 - c->u));
+        const double G1 = -q, G2 = -(D2 / S) - q * q;
+        nx = xb - (2.0 * G * G1) / (2.0 * G1 * G1 - G * G2);
+      }
+    }
     if (fabs(F) <= 16.0 * eps * (coef * asum + c->u)) {
       root = (nx >= lo && nx <= hi) ? nx : xb;
       break;

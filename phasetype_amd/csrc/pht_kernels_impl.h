@@ -470,6 +470,15 @@ __global__ void __launch_bounds__(kBlock) sweep_kernel(SweepArgs a) {
   sweep_body<NT, METHOD, DEBUG, EnvPrivate>(a, blockIdx.x, gridDim.x);
 }
 
+/* MHRS's finish (MH decisions + the accepted attempt replayed) on a
+ * persistent grid: one block per observation chunk of 256 meant ~3,900
+ * blocks at 10^6 observations, each adding its n + n^2 + extra statistics
+ * words into the same global block (~500k same-address atomics per sweep) */
+template <int NT, bool DEBUG>
+__global__ void __launch_bounds__(kBlock) mhrs_finish_kernel(SweepArgs a) {
+  sweep_body<NT, kMethodMHRS, DEBUG, EnvPrivate, true>(a, blockIdx.x, gridDim.x);
+}
+
 /* waves per SIMD the persistent kernel is compiled for: the DCS kernel at
  * n = 10 needs 410 VGPRs (one wave); held to two waves it spills 251 VGPRs
  * outside its Brent loop and runs 11 % faster (cfg5-shaped n = 10: 3.09 ->
@@ -1680,8 +1689,8 @@ template <int NT>
 __global__ void __launch_bounds__(kBlock) mhrs_finish_chains(const SweepArgs *args, int K, unsigned nblk) {
   const SweepArgs &a = args[blockIdx.x % (unsigned)K];
   const unsigned blk = blockIdx.x / (unsigned)K;
-  if ((long)blk * kBlock >= a.count) return; /* the whole block: its chain has fewer observations */
-  sweep_body<NT, kMethodMHRS, false, EnvPrivate>(a, blk, nblk);
+  if ((long)blk * kClaimChunk >= a.count) return; /* the whole block: its chain has fewer observations */
+  sweep_body<NT, kMethodMHRS, false, EnvPrivate, true>(a, blk, nblk); /* persistent (mhrs_finish_kernel) */
 }
 
 /* h: the chains' arguments on the host (sizing), d: the same K SweepArgs on
@@ -1768,7 +1777,12 @@ static hipError_t launch_chains(const SweepArgs *h, const SweepArgs *d, int K, i
     hipLaunchKernelGGL((mhrs_search_chains<NT, R4.W, R4.K>), g, dim3(kBlock), smc, st, d, K, (unsigned)nb, 4, R4.A0);
     hipLaunchKernelGGL((mhrs_compact_chains<NT>), gc, dim3(kBlock), 0, st, d, K, (unsigned)nbc, 4);
     hipLaunchKernelGGL((mhrs_search_chains<NT, R5.W, R5.K>), g, dim3(kBlock), smc, st, d, K, (unsigned)nb, 5, R5.A0);
-    const long nbf = (maxc + kBlock - 1) / kBlock;
+    static LaunchCfg cfgf;
+    int occf = 0, cusf = 0;
+    if (hipError_t e = launch_config(cfgf, (const void *)mhrs_finish_chains<NT>, smem_bytes(h[0].n), &occf, &cusf);
+        e != hipSuccess)
+      return e;
+    const long nbf = std::max(1L, std::min((maxc + kBlock - 1) / kBlock, (long)cusf * occf / K));
     hipLaunchKernelGGL((mhrs_finish_chains<NT>), dim3((unsigned)(nbf * K)), dim3(kBlock), smem_bytes(h[0].n), st, d,
                        K, (unsigned)nbf);
     return hipGetLastError();
@@ -1776,18 +1790,30 @@ static hipError_t launch_chains(const SweepArgs *h, const SweepArgs *d, int K, i
   return hipErrorInvalidValue;
 }
 
+template <int NT, bool DEBUG>
+static hipError_t launch_mhrs_finish(const SweepArgs &a, hipStream_t st) {
+  static LaunchCfg cfg;
+  const int sm = smem_bytes(a.n);
+  int occ = 0, cus = 0;
+  if (hipError_t e = launch_config(cfg, (const void *)mhrs_finish_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
+    return e;
+  long grid = (long)cus * occ;
+  const long want = (a.count + kBlock - 1) / kBlock;
+  if (grid > want) grid = want;
+  if (grid < 1) return hipSuccess;
+  hipLaunchKernelGGL((mhrs_finish_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
+  return hipGetLastError();
+}
+
 template <int NT>
 static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStream_t st) {
   if (method == kMethodECS && a.cens == nullptr) /* exact-only range */
     return debug ? launch_ecs_exact<NT, true>(a, st) : launch_ecs_exact<NT, false>(a, st);
   if (method == kMethodUNIF) return debug ? launch_unif<NT, true>(a, st) : launch_unif<NT, false>(a, st);
-  const int blocks = (int)((a.count + kBlock - 1) / kBlock);
-  if (blocks == 0) return hipSuccess;
-  const int sm = smem_bytes(a.n);
-#define PHT_LAUNCH(M, D) hipLaunchKernelGGL((sweep_kernel<NT, M, D>), dim3(blocks), dim3(kBlock), sm, st, a)
+  if (a.count <= 0) return hipSuccess;
   if (method == kMethodMHRS) {
     if (hipError_t e = launch_mhrs_search<NT>(a, st); e != hipSuccess) return e;
-    if (debug) PHT_LAUNCH(kMethodMHRS, true); else PHT_LAUNCH(kMethodMHRS, false);
+    return debug ? launch_mhrs_finish<NT, true>(a, st) : launch_mhrs_finish<NT, false>(a, st);
   } else if (method == kMethodDCS) {
     if (dcs_legacy()) {
 #ifdef PHT_LEGACY_KERNELS
@@ -1810,7 +1836,6 @@ static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStrea
     }
     return debug ? launch_cens_round<NT, true>(a, st) : launch_cens_round<NT, false>(a, st);
   }
-#undef PHT_LAUNCH
   return hipGetLastError();
 }
 
