@@ -189,6 +189,12 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
   double t = 0.0;
   int j = 0, lastj = 0, nj = 0;
   uint32_t att = 0;
+#ifdef PHT_MHRS_DIAG
+  /* diagnostic builds: wave iterations, lane iterations with an attempt, and
+   * wave iterations with at most 8 such lanes (the round's tail), all rounds
+   * (extra words 8, 9, 10) and rounds 0 / 1 (11, 12 / 13, 14) */
+  unsigned long long d_wit = 0, d_lit = 0, d_tail = 0;
+#endif
   for (;;) {
     while (!inatt) { /* next attempt of this item, or the next item */
       if (!have) {
@@ -227,6 +233,14 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
       inatt = true;
     }
     if (!__any(inatt)) break;
+#ifdef PHT_MHRS_DIAG
+    {
+      const unsigned act = (unsigned)__popcll(__ballot(inatt));
+      d_wit++;
+      d_lit += act;
+      d_tail += (act <= 8u) ? 1ull : 0ull;
+    }
+#endif
     /* converged Philox: every lane with an attempt generates its next block
      * here, once per iteration, instead of inside the draws (where only the
      * lanes whose buffer ran dry would, one draw site at a time); a step
@@ -276,6 +290,16 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
       }
     }
   }
+#ifdef PHT_MHRS_DIAG
+  if ((threadIdx.x & 63u) == 0u) {
+    unsigned long long *x = a.stats + 2 * a.n + a.n * a.n;
+    atomicAdd(&x[8], d_wit);
+    atomicAdd(&x[9], d_lit);
+    atomicAdd(&x[10], d_tail);
+    if (A0 == 0u) { atomicAdd(&x[11], d_wit); atomicAdd(&x[12], d_lit); }
+    if (A0 == kMhrsRounds[0].A0) { atomicAdd(&x[13], d_wit); atomicAdd(&x[14], d_lit); }
+  }
+#endif
 }
 
 template <int NT, int W, int K>
