@@ -16,6 +16,9 @@ run cfg3_ecs --n 20 --N 100000 --steps 20
 run cfg4_ecs --n 10 --N 1000000 --steps 20
 run cfg4_mhrs --n 10 --N 1000000 --method MHRS --steps 100
 run cfg5_mhrs --n 15 --N 500000 --censor 0.3 --method MHRS --steps 100
+# past burn-in (MHRS's attempt count follows the draw: profiles/r04/steady/)
+run cfg4_mhrs_steady --n 10 --N 1000000 --method MHRS --warmup 200 --steps 100
+run cfg5_mhrs_steady --n 15 --N 500000 --censor 0.3 --method MHRS --warmup 200 --steps 100
 run cfg5_dcs --n 15 --N 500000 --censor 0.3 --method DCS --steps 50
 run cfg5_ecs --n 15 --N 500000 --censor 0.3 --method ECS --steps 10
 run cfg3_unif --n 20 --N 100000 --method UNIF --steps 50
