@@ -193,6 +193,25 @@ def test_dcs_halley_root_matches_find02(orc, n):
     assert a["stats"][1] > 2.2 * b["stats"][1], (a["stats"][1], b["stats"][1])
 
 
+@pytest.mark.parametrize("n,cf", [(10, 0.0), (15, 0.3)])
+def test_dcs_halley_wavefront_maximum(orc, n, cf):
+    """A jump-converged DCS round waits for its slowest lane: the expected
+    maximum over 64 lanes of the Halley root's evaluations per jump
+    (tools/dcs_halley_hist.py).  r03's stop bound left ~3 % of jumps
+    bisecting at the noise floor (E[max] ~9.9); r04's bound and log-survival
+    first step bring it to ~4.7.  Guards both changes."""
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 6000, seed=90 + n, censor_frac=cf)
+    orc.halley_hist()
+    orc.dev_sweep(4, S, s, y, cen, key=(0xE1, n), sweep=1, per_obs=False)
+    h = orc.halley_hist().astype(float)
+    p = h / h.sum()
+    cdf = np.cumsum(p)
+    mean = float((np.arange(64) * p).sum())
+    emax = float(sum(1.0 - cdf[k] ** 64 for k in range(64)))
+    assert mean < 3.45 and emax < 5.0, (mean, emax)
+
+
 def test_censored_expectations_by_forward_simulation():
     """The censored analytics above against brute-force forward simulation
     conditioned on Y > y (the survey's censored probe)."""
