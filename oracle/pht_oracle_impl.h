@@ -1009,12 +1009,12 @@ static double ORC_FN(hob_halley)(const ORC_FN(hob_ctx) *c, double es, int *nev) 
         dl = Sll - ev;
         Jm = (Ei + ei) * fabs(1.0 / (ev - Sll)); /* |J_i| before E_i - e_i cancels */
       }
-      const double q = sp->Q[c->j + i * n], qb = c->Qb[i];
-      const double qJ = q * Ji, qe = q * ei;
-      tmp = fma(qJ, qb, tmp);
-      asum = fma(fabs(q) * Jm, fabs(qb), asum);
-      dtmp = fma(qe, qb, dtmp);
-      d2 = fma(qe * dl, qb, d2);
+      const double w = sp->Q[c->j + i * n] * c->Qb[i]; /* the jump's weight Q_ji Qb_i */
+      const double we = w * ei;
+      tmp = fma(w, Ji, tmp);
+      asum = fma(fabs(w), Jm, asum);
+      dtmp = fma(w, ei, dtmp);
+      d2 = fma(we, dl, d2);
     }
     (*nev)++;
     const double F = coef * tmp - c->u, D = coef * dtmp, D2 = coef * d2;

@@ -151,6 +151,15 @@ struct DcsE<NT, true> {
   __device__ __forceinline__ void set(int i, double x) { p[i * kBlock] = x; }
 };
 
+/* the jump's Halley weights w_i = Q_{jn,i} Qinv_{i,b} (fixed for the whole
+ * root search) in a lane-interleaved LDS column at n = 10: n conflict-free
+ * reads per evaluation instead of 2n gathers of two parameter rows.  At
+ * n = 15 the column (30 KB per block) would cost the second block per CU,
+ * so w_i is formed in each evaluation there and at n = 20 (the same
+ * product, the same value) */
+template <int NT>
+constexpr bool dcs_w_in_lds() { return NT == 10; }
+
 constexpr int kDcsRootMax = 1000;
 /* in the unrolled n-term loops of the n >= 10 kernels: keep the scheduler
  * from interleaving more than 4 exponentials at once (each holds ~6 double
@@ -160,9 +169,13 @@ constexpr int kDcsRootMax = 1000;
 template <int NT>
 __device__ __forceinline__ double hob_halley(const Par<NT> &P, const DcsE<NT> &E, const PHT_LDS double *rv, unsigned near,
                                              double Sjj, double X, double es, double coef, double u, int jn, int b,
-                                             Lane &ln) {
+                                             PHT_LDS double *wl, Lane &ln) {
   const int n = P.n();
   const double eps = 2.2204460492503131e-16;
+  if constexpr (dcs_w_in_lds<NT>()) {
+#pragma unroll
+    for (int i = 0; i < n; i++) wl[i * kBlock] = P.Q(jn, i) * P.Qinv(i, b);
+  }
   double lo = 0.0, hi = X;
   const double x0 = pht_log(1.0 - u * (1.0 - es)) / Sjj;
   double xb = (x0 > lo && x0 < hi) ? x0 : u * X;
@@ -185,12 +198,14 @@ __device__ __forceinline__ double hob_halley(const Par<NT> &P, const DcsE<NT> &E
         dl = Sjj - ev;
         Jm = (Ei + ei) * fabs(rv[i]); /* |J_i| before E_i - e_i cancels */
       }
-      const double q = P.Q(jn, i), qb = P.Qinv(i, b);
-      const double qJ = q * Ji, qe = q * ei;
-      tmp = fma(qJ, qb, tmp);
-      asum = fma(fabs(q) * Jm, fabs(qb), asum);
-      dtmp = fma(qe, qb, dtmp);
-      d2 = fma(qe * dl, qb, d2);
+      double w;
+      if constexpr (dcs_w_in_lds<NT>()) w = wl[i * kBlock];
+      else w = P.Q(jn, i) * P.Qinv(i, b);
+      const double we = w * ei;
+      tmp = fma(w, Ji, tmp);
+      asum = fma(fabs(w), Jm, asum);
+      dtmp = fma(w, ei, dtmp);
+      d2 = fma(we, dl, d2);
       PHT_DCS_CHUNK(i);
     }
     ln.nbrent++;
@@ -279,7 +294,7 @@ __host__ __device__ constexpr int dcs_rinv_offset(int pbytes, int n) {
 __host__ __device__ constexpr int dcs_e_offset(int pbytes, int n) { return dcs_rinv_offset(pbytes, n) + 8 * n * n; }
 template <int NT>
 constexpr int dcs_smem_bytes(int pbytes, int n) {
-  return dcs_e_offset(pbytes, n) + (dcs_e_in_lds<NT>() ? 8 * n * kBlock : 0);
+  return dcs_e_offset(pbytes, n) + (dcs_e_in_lds<NT>() ? 8 * n * kBlock : 0) + (dcs_w_in_lds<NT>() ? 8 * n * kBlock : 0);
 }
 
 /* per-lane path state between jumps */
@@ -317,6 +332,10 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
   PHT_LDS double *rinv = (PHT_LDS double *)(lsm + dcs_rinv_offset(pbytes, n));
   DcsE<NT> e;
   if constexpr (dcs_e_in_lds<NT>()) e.p = (PHT_LDS double *)(lsm + dcs_e_offset(pbytes, n)) + threadIdx.x;
+  /* the Halley weights' column (after the E rows) */
+  PHT_LDS double *wl = nullptr;
+  if constexpr (dcs_w_in_lds<NT>())
+    wl = (PHT_LDS double *)(lsm + dcs_e_offset(pbytes, n) + 8 * n * kBlock) + threadIdx.x;
   pht_stage_math_tables();
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
@@ -534,7 +553,7 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
           const int jn = st.j;
           double root;
           if (!a.dcsbrent) {
-            root = hob_halley<NT>(P, E, rinv + j * n, near, Sjj, x, es, coef, u, jn, st.b, ln);
+            root = hob_halley<NT>(P, E, rinv + j * n, near, Sjj, x, es, coef, u, jn, st.b, wl, ln);
           } else {
           /* find02(0, y - t, -u, 1 - u, HobCDF, Tol = 0, Maxit = 1000) */
           BrentSt bs;

@@ -125,13 +125,30 @@ __device__ __forceinline__ long claim_pos(long t) { return claim_pos(t, blockIdx
  * depend on which lane tried what.  mhrs_finish then makes the MH decisions
  * (tag-0 stream) and replays the accepted attempt for the statistics.
  */
+#ifndef PHT_MHRS_SCHED
+#define PHT_MHRS_SCHED 0
+#endif
+#if PHT_MHRS_SCHED == 4
+constexpr int kMhrsK0 = 8;
+#else
 constexpr int kMhrsK0 = 16;
+#endif
 struct MhrsRound {
   int W, K;
   uint32_t A0;
 };
 constexpr MhrsRound kMhrsRounds[5] = {
+#if PHT_MHRS_SCHED == 1 /* A/B: shorter items (K = 8), twice the lanes per task */
+    {16, 8, 16}, {128, 8, 144}, {2048, 8, 1168}, {32768, 8, 17552}, {131072, 32, 279696}};
+#elif PHT_MHRS_SCHED == 3 /* A/B: K = 4 */
+    {32, 4, 16}, {256, 4, 144}, {4096, 4, 1168}, {65536, 4, 17552}, {131072, 32, 279696}};
+#elif PHT_MHRS_SCHED == 4 /* A/B: round 0 K0 = 8, then K = 8 */
+    {16, 8, 8}, {128, 8, 136}, {2048, 8, 1160}, {32768, 8, 17544}, {131072, 32, 279688}};
+#elif PHT_MHRS_SCHED == 2 /* A/B: longer items (K = 32), half the lanes per task */
+    {4, 32, 16}, {32, 32, 144}, {512, 32, 1168}, {8192, 32, 17552}, {131072, 32, 279696}};
+#else
     {8, 16, 16}, {64, 16, 144}, {1024, 16, 1168}, {16384, 16, 17552}, {131072, 32, 279696}};
+#endif
 
 template <int NT>
 __device__ __forceinline__ Par<NT> stage_params(const SweepArgs &a, PHT_LDS unsigned char *lsm) {
@@ -1332,9 +1349,12 @@ namespace pht {
 #ifndef PHT_DCS_WAVES
 #define PHT_DCS_WAVES 0
 #endif
+/* n = 20: the block's LDS (parameters, reciprocals and the E rows, 82 KB)
+ * allows one block per CU, so the kernel is compiled for one wave per SIMD
+ * (it spilled 141 VGPRs holding to two it could never get) */
 template <int NT>
 constexpr int dcs_waves() {
-  return PHT_DCS_WAVES > 0 ? PHT_DCS_WAVES : 2;
+  return PHT_DCS_WAVES > 0 ? PHT_DCS_WAVES : (NT == 20 ? 1 : 2);
 }
 template <int NT, bool DEBUG>
 __global__ void __launch_bounds__(kBlock)
