@@ -117,8 +117,8 @@ __device__ __forceinline__ long claim_pos(long t) { return claim_pos(t, blockIdx
  * (a few tasks per sweep need ~1e5-1e6 attempts, the reference's whole
  * run time; one lane per observation would serialise them):
  *   round 0  one lane per task, attempts [0, 16)
- *   round r  W = 8, 64, 1024, 16384, 131072 lanes per unresolved task,
- *            K = 16 (32) attempts each: attempt A0 + l + W k for lane l
+ *   round r  W = 16, 128, 2048, 32768, 131072 lanes per unresolved task,
+ *            K = 8 (32) attempts each: attempt A0 + l + W k for lane l
  * (mhrs_search: jump-converged, the tasks' records lowered by atomicMin;
  * mhrs_compact collects the unresolved tasks between rounds).
  * Attempt streams are per (task, attempt), so the first success does not
@@ -137,17 +137,22 @@ struct MhrsRound {
   int W, K;
   uint32_t A0;
 };
+/* rounds 1-4 with K = 8 attempts per item (r04; r03 had K = 16 and half the
+ * lanes per task): shorter items leave shorter round tails.  Interleaved A/B
+ * (profiles/r04/mhrs_ab/sched_*.json): cfg4 -1 %, cfg5 -19 %; K = 4 or
+ * round 0 at 8 attempts gained at cfg5 but lost 8-15 % at cfg4, K = 32 lost
+ * 26 %.  (PHT_MHRS_SCHED selects the alternatives in variant builds.) */
 constexpr MhrsRound kMhrsRounds[5] = {
-#if PHT_MHRS_SCHED == 1 /* A/B: shorter items (K = 8), twice the lanes per task */
+#if PHT_MHRS_SCHED == 0
     {16, 8, 16}, {128, 8, 144}, {2048, 8, 1168}, {32768, 8, 17552}, {131072, 32, 279696}};
+#elif PHT_MHRS_SCHED == 1 /* r03's schedule */
+    {8, 16, 16}, {64, 16, 144}, {1024, 16, 1168}, {16384, 16, 17552}, {131072, 32, 279696}};
 #elif PHT_MHRS_SCHED == 3 /* A/B: K = 4 */
     {32, 4, 16}, {256, 4, 144}, {4096, 4, 1168}, {65536, 4, 17552}, {131072, 32, 279696}};
 #elif PHT_MHRS_SCHED == 4 /* A/B: round 0 K0 = 8, then K = 8 */
     {16, 8, 8}, {128, 8, 136}, {2048, 8, 1160}, {32768, 8, 17544}, {131072, 32, 279688}};
-#elif PHT_MHRS_SCHED == 2 /* A/B: longer items (K = 32), half the lanes per task */
+#else /* 2, A/B: longer items (K = 32), half the lanes per task */
     {4, 32, 16}, {32, 32, 144}, {512, 32, 1168}, {8192, 32, 17552}, {131072, 32, 279696}};
-#else
-    {8, 16, 16}, {64, 16, 144}, {1024, 16, 1168}, {16384, 16, 17552}, {131072, 32, 279696}};
 #endif
 
 template <int NT>
