@@ -367,7 +367,7 @@ struct pht_ctx {
    * law by uniformisation (PHT_MHRS=bridge, PHT_DCS=bridge; pht_unif.h) */
   int rmethod = 0, ulaw = 0;
   long count = 0;
-  long n_exact = 0;                      /* observations [0, n_exact) are exact (sorted first) */
+  long n_exact = 0;                      /* exact observations; ECS: positions [0, n_exact) (sorted first) */
   double *d_y = nullptr;
   int *d_cens = nullptr;
   uint32_t *d_gid = nullptr;
@@ -902,13 +902,22 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
   if (count == 0) return 0;
   std::vector<long> ord(count);
   std::iota(ord.begin(), ord.end(), 0L);
-  /* exact observations, then censored ones, each by decreasing y: the
-   * persistent kernels hand out long paths first and end on short ones (a
-   * short tail).  PHT_ORDER=asc|none: A/B of the exact range. */
+  /* by decreasing y, so the persistent kernels hand out long paths first
+   * and end on short ones (a short tail).  Exact observations first, then
+   * censored ones, each by decreasing y: ECS runs the two as ranges of their
+   * own (two kernels, two streams), and MHRS's and UNIF's code paths differ
+   * for censored observations (a wavefront of one kind does not diverge).
+   * DCS treats censored observations as exact (the reference's DCS law), so
+   * its one kernel takes the whole shard by decreasing y (r04: the censored
+   * range's long paths started two thirds of the way through the kernel and
+   * set its tail; cfg5 DCS 1.19 -> 0.89 ms).  PHT_ORDER=asc|none: A/B of
+   * ECS's exact range. */
+  const bool split = !(c->method == kMethodDCS || (c->method == kMethodUNIF && c->ulaw == 2));
   const char *oe = getenv("PHT_ORDER");
   const int omode = !oe ? 0 : (!strcmp(oe, "asc") ? 1 : (!strcmp(oe, "none") ? 2 : 0));
   std::stable_sort(ord.begin(), ord.end(), [&](long a, long b) {
     const int ca = cens[a] != 0, cb = cens[b] != 0;
+    if (!split) return y[a] > y[b];
     if (ca != cb) return ca < cb;
     if (ca) return y[a] > y[b];
     if (omode == 2) return false;
@@ -923,7 +932,11 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
     gs[k] = (uint32_t)(obs0 + ord[k]);
   }
   c->n_exact = 0;
-  while (c->n_exact < count && cs[c->n_exact] == 0) c->n_exact++;
+  if (split) {
+    while (c->n_exact < count && cs[c->n_exact] == 0) c->n_exact++;
+  } else {
+    for (long k = 0; k < count; k++) c->n_exact += (cs[k] == 0); /* (not a range here) */
+  }
   c->h_ysorted = ys;
   c->ysum = 0.0;
   c->ymax = 0.0;
