@@ -1100,6 +1100,12 @@ static int ctx_launch(pht_ctx *c, const SweepArgs &a, bool debug) {
      * work; cfg5 ECS 2.49 -> 1.92 ms; the launch order does not matter
      * (PHT_CENS_SERIAL=1: one stream) */
     const bool fork = ae.count > 0 && ac.count > 0 && !getenv("PHT_CENS_SERIAL");
+    /* n >= 15: the exact kernel's LDS now allows two blocks per CU (compact
+     * parameter prefix, r04), which pays alone (n = 15, 5e5 exact: 1.178 ->
+     * 1.038 ms) but crowds out the concurrent censored kernel (cfg5: 1.224
+     * -> 1.482 ms; profiles/r04/ecs_lds/): with a censored range running
+     * beside it, one block per CU as before */
+    if (fork && c->n >= 15 && !getenv("PHT_ECS_OCC")) ae.occ = 1;
     if (fork) {
       HIPCHK(hipEventRecord(c->evf, c->stream));
       HIPCHK(hipStreamWaitEvent(c->stream2, c->evf, 0));

@@ -628,6 +628,31 @@ static hipError_t launch_persist(const SweepArgs &a, hipStream_t st) {
 #ifndef PHT_SLOW_K
 #define PHT_SLOW_K 15
 #endif
+/* envelope points kept in LDS (lane-interleaved x and y; beyond them the
+ * general ARMS code's rare long envelopes go to private memory).  At
+ * n >= 15 only the converged round's 13 (with the compact parameter prefix
+ * below, two blocks per CU then fit at n = 15 and 20) */
+template <int NT>
+constexpr int ecs_env_k() { return NT >= 15 ? 13 : PHT_SLOW_K; }
+
+/* The ECS exact-path kernels (one-lane, rows, chains, hand-off) stage into
+ * LDS only what they read: the parameter block's double prefix [0, necs)
+ * (the n-vectors, S, P, QQs, W, the W moments) and P's successor lists,
+ * which follow it in LDS (P.iv).  The full block (22 KB at n = 15) plus the
+ * envelope region and the math tables exceeded half of the CU's 160 KB, so
+ * the n = 15 and 20 kernels ran one block, i.e. one wave per SIMD (r04). */
+__host__ __device__ inline int ecs_param_bytes(const Layout &L) {
+  return L.necs * 8 + (((L.n + L.n * L.n) * 4 + 15) & ~15);
+}
+__device__ __forceinline__ void stage_ecs_params(const SweepArgs &a, PHT_LDS unsigned char *lsm, const Layout &L) {
+  const unsigned long long *g = reinterpret_cast<const unsigned long long *>(a.params);
+  PHT_LDS unsigned long long *d = (PHT_LDS unsigned long long *)lsm;
+  for (int k = threadIdx.x; k < L.necs; k += blockDim.x) d[k] = g[k];
+  const int *gi = reinterpret_cast<const int *>(reinterpret_cast<const unsigned char *>(a.params) + L.ndouble * 8);
+  PHT_LDS int *di = (PHT_LDS int *)(lsm + L.necs * 8);
+  const int ni = L.n + L.n * L.n; /* nsuccP, succP: the int region's prefix */
+  for (int k = threadIdx.x; k < ni; k += blockDim.x) di[k] = gi[k];
+}
 
 #ifndef PHT_ECS_WAVES
 #define PHT_ECS_WAVES 0
@@ -640,12 +665,8 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
   const Layout L = make_layout(n);
-  const int pbytes = L.bytes();
-  {
-    const unsigned long long *src = reinterpret_cast<const unsigned long long *>(a.params);
-    PHT_LDS unsigned long long *dst = (PHT_LDS unsigned long long *)smem;
-    for (int k = threadIdx.x; k < pbytes / 8; k += blockDim.x) dst[k] = src[k];
-  }
+  const int pbytes = ecs_param_bytes(L);
+  stage_ecs_params(a, (PHT_LDS unsigned char *)smem, L);
   PHT_LDS unsigned char *lsm = (PHT_LDS unsigned char *)smem;
   PHT_LDS unsigned long long *zq = (PHT_LDS unsigned long long *)(lsm + pbytes);
   PHT_LDS unsigned long long *xc = zq + n;
@@ -661,13 +682,13 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
 
   Par<NT> P;
   P.d = (const PHT_LDS double *)lsm;
-  P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
+  P.iv = (const PHT_LDS int *)(lsm + L.necs * 8);
   P.Lr = L;
   /* the envelope's x and y in LDS (lane-interleaved) up to PHT_SLOW_K
    * points; cum lives in registers within a round (pht_ecs_round.h) and in
    * private memory for the general ARMS code */
-  EnvLdsXY<PHT_SLOW_K, kBlock> env;
-  double spill[2 * EnvLdsXY<PHT_SLOW_K, kBlock>::kSpill];
+  EnvLdsXY<ecs_env_k<NT>(), kBlock> env;
+  double spill[2 * EnvLdsXY<ecs_env_k<NT>(), kBlock>::kSpill];
   double cumv[100];
   env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill, (PHT_PRIV double *)cumv);
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
@@ -937,12 +958,8 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
   extern __shared__ __align__(16) unsigned char smem[];
   constexpr int n = NT;
   const Layout L = make_layout(n);
-  const int pbytes = L.bytes();
-  {
-    const unsigned long long *src = reinterpret_cast<const unsigned long long *>(a.params);
-    PHT_LDS unsigned long long *dst = (PHT_LDS unsigned long long *)smem;
-    for (int k = threadIdx.x; k < pbytes / 8; k += blockDim.x) dst[k] = src[k];
-  }
+  const int pbytes = ecs_param_bytes(L);
+  stage_ecs_params(a, (PHT_LDS unsigned char *)smem, L);
   PHT_LDS unsigned char *lsm = (PHT_LDS unsigned char *)smem;
   PHT_LDS unsigned long long *zq = (PHT_LDS unsigned long long *)(lsm + pbytes);
   PHT_LDS unsigned long long *xc = zq + n;
@@ -963,7 +980,7 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
 
   Par<NT> P;
   P.d = (const PHT_LDS double *)lsm;
-  P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
+  P.iv = (const PHT_LDS int *)(lsm + L.necs * 8);
   P.Lr = L;
   const RowId<NT> id = row_id<NT>(P, (int)(threadIdx.x & (kRowW - 1)));
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
@@ -1169,13 +1186,16 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
  * at n = 10 with row blocks (the row code would otherwise take it to one)
  * and at n = 15, where the
  * W row read from LDS (EcsDens) lets it fit (255 VGPRs, no spills, per the
- * built library's metadata: tools/kernel_regs.py); otherwise what the
- * registers allow (PHT_ECS_WAVES=k forces every n).  The DEBUG=true
+ * built library's metadata: tools/kernel_regs.py); at n = 20 two as well
+ * since the compact parameter prefix lets two blocks share a CU (r04: 43
+ * spilled VGPRs in the one-lane body, cfg3 kernel 0.858 -> 0.824 ms in an
+ * interleaved A/B); otherwise what the registers allow (PHT_ECS_WAVES=k
+ * forces every n).  The DEBUG=true
  * instantiations (per-observation outputs for the parity tests) may spill a
  * few VGPRs: they are never timed. */
 template <int NT, bool ROWS = false>
 constexpr int ecs_waves() {
-  return PHT_ECS_WAVES > 0 ? PHT_ECS_WAVES : ((NT == 15 || (ROWS && NT == 10)) ? 2 : 1);
+  return PHT_ECS_WAVES > 0 ? PHT_ECS_WAVES : ((NT == 15 || NT == 20 || (ROWS && NT == 10)) ? 2 : 1);
 }
 template <int NT, bool DEBUG, bool ROWS, bool HAND = false>
 __global__ void __launch_bounds__(kBlock)
@@ -1226,14 +1246,17 @@ ecs_chains_kernel(const SweepArgs *args, int K, unsigned nblk) {
   ecs_exact_body<NT, false>(a, blockIdx.x / (unsigned)K, nblk);
 }
 
+template <int NT>
 static int smem_bytes_ecs(int n) {
-  return ((smem_bytes(n) + 4 + 15) & ~15) + 2 * PHT_SLOW_K * 8 * kBlock;
+  const Layout L = make_layout(n);
+  return ((ecs_param_bytes(L) + (n + kStatExtra) * 8 + (n + n * n) * 4 + 4 + 4 + 15) & ~15) +
+         2 * ecs_env_k<NT>() * 8 * kBlock;
 }
 
 template <int NT, bool DEBUG>
 static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
   static LaunchCfg cfg, cfgr, cfgh;
-  const int sm = smem_bytes_ecs(a.n);
+  const int sm = smem_bytes_ecs<NT>(a.n);
   const bool rows = row_ok<NT>() && a.rowk > 0;
   const bool hand = rows && a.hand > 0;
   const void *kfn = hand   ? (const void *)ecs_exact_kernel<NT, DEBUG, row_ok<NT>(), true>
@@ -1288,7 +1311,7 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
 template <int NT>
 static hipError_t launch_ecs_chains(const SweepArgs *h, const SweepArgs *d, int K, hipStream_t st) {
   static LaunchCfg cfg;
-  const int sm = smem_bytes_ecs(h[0].n);
+  const int sm = smem_bytes_ecs<NT>(h[0].n);
   int occ = 0, cus = 0;
   if (hipError_t e = launch_config(cfg, (const void *)ecs_chains_kernel<NT>, sm, &occ, &cus); e != hipSuccess)
     return e;

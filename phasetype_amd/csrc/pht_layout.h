@@ -40,6 +40,7 @@ struct Layout {
   int n;
   /* f64 offsets (in doubles) */
   int evals, s, logs, scale, logscale, piQ, pi, S, P, Pf, QQs, W, QQ1, V, Q, Qinv, Wm, ndouble;
+  int necs; /* doubles the ECS exact path reads: a prefix of the block */
   /* int32 offsets (in ints, from the start of the int region) */
   int nsuccP, succP, nsuccPf, succPf, nsuccS, succS, nint;
   PHT_LHD int bytes() const { return ndouble * 8 + nint * 4; }
@@ -58,14 +59,18 @@ PHT_LHD Layout make_layout(int n) {
   L.pi = o; o += n;
   L.S = o; o += nn;
   L.P = o; o += nn;
-  L.Pf = o; o += nn + n;
   L.QQs = o; o += nn;
   L.W = o; o += nn;
+  L.Wm = o; o += 6 * n;
+  o += (o & 1);
+  /* [0, necs): everything the ECS exact-path kernels read (r04); they stage
+   * only this prefix and P's successor lists, see stage_ecs_params */
+  L.necs = o;
+  L.Pf = o; o += nn + n;
   L.QQ1 = o; o += nn;
   L.V = o; o += nn;
   L.Q = o; o += nn;
   L.Qinv = o; o += nn;
-  L.Wm = o; o += 6 * n;
   o += (o & 1); /* keep the int region 16-byte aligned */
   L.ndouble = o;
   int k = 0;

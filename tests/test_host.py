@@ -121,8 +121,11 @@ def _layout(n):
     nn = n * n
     o, L = 0, {}
     for name, size in (("evals", n), ("s", n), ("logs", n), ("scale", n), ("logscale", n), ("piQ", n), ("pi", n),
-                       ("S", nn), ("P", nn), ("Pf", nn + n), ("QQs", nn), ("W", nn), ("QQ1", nn), ("V", nn),
-                       ("Q", nn), ("Qinv", nn), ("Wm", 6 * n)):
+                       ("S", nn), ("P", nn), ("QQs", nn), ("W", nn), ("Wm", 6 * n)):
+        L[name] = (o, size)
+        o += size
+    o += o & 1  # the ECS exact path's prefix ends here (Layout::necs)
+    for name, size in (("Pf", nn + n), ("QQ1", nn), ("V", nn), ("Q", nn), ("Qinv", nn)):
         L[name] = (o, size)
         o += size
     o += o & 1
