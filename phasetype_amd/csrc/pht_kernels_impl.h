@@ -130,6 +130,10 @@ __device__ __forceinline__ long claim_pos(long t) { return claim_pos(t, blockIdx
 #endif
 #if PHT_MHRS_SCHED == 4
 constexpr int kMhrsK0 = 8;
+#elif PHT_MHRS_SCHED == 5
+constexpr int kMhrsK0 = 32;
+#elif PHT_MHRS_SCHED == 6
+constexpr int kMhrsK0 = 24;
 #else
 constexpr int kMhrsK0 = 16;
 #endif
@@ -151,6 +155,10 @@ constexpr MhrsRound kMhrsRounds[5] = {
     {32, 4, 16}, {256, 4, 144}, {4096, 4, 1168}, {65536, 4, 17552}, {131072, 32, 279696}};
 #elif PHT_MHRS_SCHED == 4 /* A/B: round 0 K0 = 8, then K = 8 */
     {16, 8, 8}, {128, 8, 136}, {2048, 8, 1160}, {32768, 8, 17544}, {131072, 32, 279688}};
+#elif PHT_MHRS_SCHED == 5 /* A/B: round 0 K0 = 32 */
+    {16, 8, 32}, {128, 8, 160}, {2048, 8, 1184}, {32768, 8, 17568}, {131072, 32, 279712}};
+#elif PHT_MHRS_SCHED == 6 /* A/B: round 0 K0 = 24 */
+    {16, 8, 24}, {128, 8, 152}, {2048, 8, 1176}, {32768, 8, 17560}, {131072, 32, 279704}};
 #else /* 2, A/B: longer items (K = 32), half the lanes per task */
     {4, 32, 16}, {32, 32, 144}, {512, 32, 1168}, {8192, 32, 17552}, {131072, 32, 279696}};
 #endif
