@@ -66,3 +66,27 @@ def test_ecs_debug_instantiations(regs, nt):
     assert len(hits) == 1, (key, list(hits))
     (name, d), = hits.items()
     assert d["vgpr_spill"] <= 96, (name, d)
+
+
+def _ecs_dynamic_lds(n, env_k):
+    """phasetype_amd/csrc/pht_kernels_impl.h smem_bytes_ecs: the parameter
+    block's ECS prefix (Layout::necs doubles) + P's successor lists, the
+    statistics and cursor, then the lane-interleaved envelope (x, y)."""
+    nn = n * n
+    necs = 7 * n + 4 * nn + 6 * n
+    necs += necs & 1
+    pbytes = necs * 8 + (((n + nn) * 4 + 15) & ~15)
+    return ((pbytes + (n + 16) * 8 + (n + nn) * 4 + 4 + 4 + 15) & ~15) + 2 * env_k * 8 * 256
+
+
+@pytest.mark.parametrize("nt,env_k", [(10, 15), (15, 13), (20, 13)])
+def test_ecs_two_blocks_per_cu(regs, nt, env_k):
+    """Two ECS blocks (two waves per SIMD) must fit one CU's 160 KB of LDS:
+    until r04 the n = 15 and 20 kernels staged the whole parameter block with
+    a 15-point envelope and ran ONE block per CU (DESIGN.md §0c,
+    profiles/r04/ecs_lds/)."""
+    key = f"ecs_exact_kernelILi{nt}ELb0ELb0ELb0E"
+    (name, d), = {k: v for k, v in regs.items() if key in k}.items()
+    per_block = _ecs_dynamic_lds(nt, env_k) + int(d["lds_static"])
+    assert 2 * per_block <= 160 * 1024, (name, per_block)
+    assert d["waves_per_simd"] >= 2, (name, d)
