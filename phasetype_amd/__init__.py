@@ -140,6 +140,11 @@ def stats_len(n: int) -> int:
     return 2 * n + n * n + 16
 
 
+# extra-word indices (phasetype_amd/csrc/pht_layout.h): the ECS exact
+# kernels' DEBUG launches count general-ARMS and private-envelope rounds there
+XDBG_GENERAL, XDBG_PRIVATE = 8, 9
+
+
 def split_stats(st, n):
     """int64 block -> (zq[n], B[n], N[n,n] as N[from, to], extras[16])."""
     st = np.asarray(st)

@@ -769,6 +769,11 @@ extern "C" int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id, int nran
   return 0;
 }
 
+#ifdef PHT_HANDOFF
+/* present only in -D PHT_HANDOFF variant builds (the hand-off tests look for it) */
+extern "C" int pht_variant_handoff(void) { return 1; }
+#endif
+
 /* in-place sum of a host int64 vector over the context's communicator, on its
  * stream (the same all-reduce a sweep runs on its statistics block): the
  * attach-time self-test of phasetype_amd/dist.py compares it with
@@ -777,17 +782,28 @@ extern "C" int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id, int nran
  * the all-reduce, even when its upload failed (the error is reported after
  * the collective), so its peers are never left waiting. */
 extern "C" int pht_ctx_rccl_allreduce(pht_ctx *c, long long *buf, int len) {
-  if (!c || !c->comm || !buf || len < 1 || len > c->rccl_cap) {
-    set_err("pht_ctx_rccl_allreduce: need a context with an RCCL communicator and 1 <= len <= the prepared size");
+  if (!c || !c->comm) {
+    set_err("pht_ctx_rccl_allreduce: need a context with an RCCL communicator");
     return -1;
   }
+  /* a bad length on this rank alone must not leave the peers inside the
+   * collective: it still enters it, with the prepared size clamped (zeros
+   * where it has no data), and reports the error afterwards */
+  const bool badlen = !buf || len < 1 || len > c->rccl_cap;
+  const int nred = badlen ? std::max(1, std::min(len, c->rccl_cap)) : len;
   (void)hipSetDevice(c->device);
-  hipError_t e = hipMemcpyAsync(c->d_rccl, buf, sizeof(long long) * len, hipMemcpyHostToDevice, c->stream);
-  const ncclResult_t r = rccl().allReduce(c->d_rccl, c->d_rccl, (size_t)len, ncclUint64, ncclSum, c->comm, c->stream);
-  if (e == hipSuccess && r == ncclSuccess)
+  hipError_t e = hipMemsetAsync(c->d_rccl, 0, sizeof(long long) * nred, c->stream);
+  if (e == hipSuccess && !badlen)
+    e = hipMemcpyAsync(c->d_rccl, buf, sizeof(long long) * len, hipMemcpyHostToDevice, c->stream);
+  const ncclResult_t r = rccl().allReduce(c->d_rccl, c->d_rccl, (size_t)nred, ncclUint64, ncclSum, c->comm, c->stream);
+  if (e == hipSuccess && r == ncclSuccess && !badlen)
     e = hipMemcpyAsync(buf, c->d_rccl, sizeof(long long) * len, hipMemcpyDeviceToHost, c->stream);
   const hipError_t es = hipStreamSynchronize(c->stream);
   if (e == hipSuccess) e = es;
+  if (badlen) {
+    set_err("pht_ctx_rccl_allreduce: need 1 <= len <= the prepared size (%d), got %d", c->rccl_cap, len);
+    return -1;
+  }
   if (r != ncclSuccess) {
     set_err("RCCL all-reduce failed: %s", rccl().errStr(r));
     return -1;
@@ -967,15 +983,18 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
     const bool pre = e ? atoi(e) != 0 : count >= kDcsPrepassMin;
     if (c->method == kMethodDCS && pre) HIPCHK(hipMalloc(&c->d_dcsb, sizeof(int) * count));
   }
-  /* ECS hand-off records: one per exact observation at most (each is handed
-   * off at most once), where the policy can turn it on */
-  if (c->method == kMethodECS && c->n_exact > 0 && (c->n_exact <= 2 * kSpreadLanes || getenv("PHT_HAND"))) {
+#ifdef PHT_HANDOFF
+  /* ECS hand-off records (a -D PHT_HANDOFF variant build only, when PHT_HAND
+   * asks for it): one per exact observation at most (each is handed off at
+   * most once) */
+  if (c->method == kMethodECS && c->n_exact > 0 && getenv("PHT_HAND") && atoi(getenv("PHT_HAND")) > 0) {
     HIPCHK(hipMalloc(&c->d_cbuf, sizeof(EcsCont) * c->n_exact));
     HIPCHK(hipMalloc(&c->d_cready, sizeof(unsigned) * c->n_exact));
     HIPCHK(hipMalloc(&c->d_cq, sizeof(unsigned) * kContQ));
     HIPCHK(hipMemset(c->d_cready, 0, sizeof(unsigned) * c->n_exact));
     c->cont_cap = c->n_exact;
   }
+#endif
   return 0;
 }
 
@@ -1011,6 +1030,10 @@ static long exact_rowk(const pht_ctx *c) {
  * one-lane path still running after this many jumps continues on a row.
  * PHT_HAND=k forces it (0 = off) */
 static int exact_hand(const pht_ctx *c) {
+#ifndef PHT_HANDOFF
+  (void)c;
+  return 0; /* the experimental hand-off exists only in -D PHT_HANDOFF variant builds */
+#endif
   if (!c->d_cbuf) return 0;
   if (const char *e = getenv("PHT_HAND")) return std::max(0, atoi(e));
   return 0;
@@ -1462,8 +1485,10 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
       flagged += fl;
     }
     /* UNIF observations beyond the table or the lam cap carry a path that is
-     * not a draw of the target law (pht_unif.h): an error, not a warning */
-    if (xw[kXUnifCap] > 0) {
+     * not a draw of the target law (pht_unif.h): an error, not a warning.
+     * Only sweeps that ran the UNIF kernels: other samplers' diagnostic
+     * builds (PHT_ECS_DIAG, PHT_DCS_DIAG) count their own things in word 6 */
+    if (bm == kMethodUNIF && xw[kXUnifCap] > 0) {
       set_err("sweep %d: %lld UNIF observations need more than %d uniformisation steps or mu*y > %g (the largest "
               "exit rate times the largest observation); their paths would be wrong: rescale the data",
               iter, xw[kXUnifCap], kUnifMaxK, kUnifMaxLam);
@@ -1729,6 +1754,7 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
   ra.it = it;
   ra.init = 1;
   ra.eig = (disp == kMethodECS || disp == kMethodDCS) ? 1 : 0;
+  ra.unif = (disp == kMethodUNIF || c->ulaw) ? 1 : 0;
   ra.zs = ldexp(1.0, -zexp);
   ra.expect = c->global_count >= 0 ? c->global_count : (c->comm ? -1 : (long long)c->count);
   ra.k0 = k0;
@@ -1812,9 +1838,26 @@ extern "C" int pht_gibbs_run_resident(pht_ctx *c, int it, int method, int m, con
   for (int iter = 1; iter < it; iter++) {
     if (iter % kErrPoll == 0) {
       /* a failed sweep (e.g. the eigensystem) makes the update kernels
-       * return at entry; stop enqueueing instead of running to `it` */
-      HIPCHK(hipMemcpyAsync(&early, berr.p, sizeof early, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
+       * return at entry; stop enqueueing instead of running to `it`.  With a
+       * communicator the decision is collective (the maximum of the ranks'
+       * error words), so no rank leaves the loop while its peers still enter
+       * the per-sweep all-reduce */
+      if (c->comm && c->d_rccl) {
+        HIPCHK(hipMemsetAsync(c->d_rccl, 0, sizeof(long long), st));
+        HIPCHK(hipMemcpyAsync(c->d_rccl, berr.p, sizeof(int), hipMemcpyDeviceToDevice, st));
+        const ncclResult_t rr = rccl().allReduce(c->d_rccl, c->d_rccl, 1, ncclUint64, ncclMax, c->comm, st);
+        if (rr != ncclSuccess) {
+          set_err("RCCL all-reduce of the error word failed: %s", rccl().errStr(rr));
+          return -1;
+        }
+        long long ew = 0;
+        HIPCHK(hipMemcpyAsync(&ew, c->d_rccl, sizeof ew, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        early = (int)ew;
+      } else {
+        HIPCHK(hipMemcpyAsync(&early, berr.p, sizeof early, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+      }
       if (early) break;
     }
     a.sweep = (uint32_t)iter;

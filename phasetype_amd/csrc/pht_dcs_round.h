@@ -45,8 +45,15 @@ namespace pht {
 /* lane phases */
 enum : int { kDcsFree = 0, kDcsSetup = 1, kDcsNew = 3, kDcsDone = 4 };
 
-/* Find02's state between CDF evaluations (src/utility.c:233-338, find02 in
- * pht_device.h); tol = 0 as dcs() calls it */
+/* Provenance: brent_head/brent_tail below are Brent's zeroin as in R core's
+ * src/library/stats/src/zeroin.c (R_zeroin2; GPL-2), which the reference
+ * carries as Find02 (src/utility.c:233-338, itself that R code).  Its
+ * statement order is kept, split around the f(b) call so that a wavefront can
+ * run it as a state machine, because PHT_DCS_ROOT=brent must reproduce the
+ * reference's root bit for bit (the default root is hob_halley).
+ *
+ * Find02's state between CDF evaluations (find02 in pht_device.h); tol = 0
+ * as dcs() calls it */
 struct BrentSt {
   double a, b, c, fa, fb, fc;
   int maxit;

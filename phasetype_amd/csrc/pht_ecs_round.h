@@ -429,6 +429,7 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
       ainfo = rc;
       acc = true;
     }
+    sk.arms_diag(true, env.cnt > Env::kLds);
   }
   PHT_STAMP(ln, 10);
 #ifdef PHT_TRACE_GID

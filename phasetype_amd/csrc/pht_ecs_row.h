@@ -766,6 +766,7 @@ __device__ __forceinline__ bool row_round(const Par<NT> &P, const RowId<NT> &id,
     EcsDens<NT> f1{P, j, y_t, P.S(j, j), E0f, true, -1.0, {}, 0.0, {}};
     f1.load(id.lammax);
     const int rc = arms_step(benv, f1, pd, 0.0, xsamp, ln);
+    sk.arms_diag(id.lead, id.lead); /* the private copy, once per row */
     if (rc != 1) {
       ainfo = rc;
       acc = true;

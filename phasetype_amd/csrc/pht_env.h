@@ -27,6 +27,7 @@ namespace pht {
 
 struct EnvPrivate {
   static constexpr bool kUnroll = true; /* arms_*: unrolled code for envelopes of <= kArmsU points */
+  static constexpr int kLds = 0;        /* points held outside private memory */
   double x[100], y[100], cum[100];
   int cnt;
   double ymax;
@@ -57,6 +58,7 @@ struct EnvPrivateBig : EnvPrivate {
 template <int K, int STRIDE>
 struct EnvLdsXY {
   static constexpr bool kUnroll = true;
+  static constexpr int kLds = K;
   static constexpr int kSpill = 100 - K;
   PHT_LDS double *l;   /* lane's element 0 */
   PHT_PRIV double *ov; /* [2][kSpill] x, y beyond K */

@@ -105,6 +105,7 @@ struct SweepArgs {
 struct ResidentArgs {
   int n, m, it, init;
   int eig;                      /* ECS/DCS: the eigensystem and spectral products too (include/pht_eigen.h) */
+  int unif;                     /* the sweep runs the UNIF kernels (method 8 or a bridge mode): kXUnifCap applies */
   double zs;                    /* 2^-zexp */
   long long expect;             /* observations per sweep, node-wide (< 0: unchecked) */
   uint32_t k0, k1;              /* Philox key of the Gamma streams (include/pht_gamma.h) */

@@ -75,6 +75,7 @@ struct Sink {
   long long *dz;          /* debug row [n] */
   int *dN;                /* debug row [n*n] */
   int *dB, *dpre;
+  PHT_LDS unsigned long long *xc = nullptr; /* LDS extra words (arms_diag) */
   __device__ __forceinline__ void z(int k, double d) {
     const long long q = (long long)rint(d * zscale);
     lds_add(&zq[k], (unsigned long long)q);
@@ -90,6 +91,18 @@ struct Sink {
   }
   __device__ __forceinline__ void pre(int j) {
     if (DEBUG) *dpre = j;
+  }
+  /* DEBUG instantiations: a round in the general ARMS code, and whether its
+   * envelope reached private memory (kXDbgGeneral, kXDbgPrivate) */
+  __device__ __forceinline__ void arms_diag(bool general, bool priv) {
+#ifndef PHT_STAMPS
+    if constexpr (DEBUG) {
+      if (general) lds_add(&xc[kXDbgGeneral], 1ull);
+      if (priv) lds_add(&xc[kXDbgPrivate], 1ull);
+    }
+#else
+    (void)general; (void)priv;
+#endif
   }
 };
 
@@ -699,7 +712,7 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
   double spill[2 * EnvLdsXY<ecs_env_k<NT>(), kBlock>::kSpill];
   double cumv[100];
   env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill, (PHT_PRIV double *)cumv);
-  Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
+  Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr, xc};
   Lane ln;
 #ifdef PHT_STAMPS
   ln.st_last = __builtin_amdgcn_s_memtime();
@@ -991,7 +1004,7 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
   P.iv = (const PHT_LDS int *)(lsm + L.necs * 8);
   P.Lr = L;
   const RowId<NT> id = row_id<NT>(P, (int)(threadIdx.x & (kRowW - 1)));
-  Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
+  Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr, xc};
   Lane ln;
   RowObs<NT> st;
   st.yt = 0.0; st.j = 0; st.njump = 0; st.haveE0 = false; st.haveDen = false; st.fold = false; st.den = 0.0;
@@ -1266,10 +1279,17 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
   static LaunchCfg cfg, cfgr, cfgh;
   const int sm = smem_bytes_ecs<NT>(a.n);
   const bool rows = row_ok<NT>() && a.rowk > 0;
+#ifdef PHT_HANDOFF
   const bool hand = rows && a.hand > 0;
   const void *kfn = hand   ? (const void *)ecs_exact_kernel<NT, DEBUG, row_ok<NT>(), true>
                     : rows ? (const void *)ecs_exact_kernel<NT, DEBUG, row_ok<NT>()>
                            : (const void *)ecs_exact_kernel<NT, DEBUG, false>;
+#else
+  /* (the experimental hand-off kernels exist only in -D PHT_HANDOFF builds) */
+  const bool hand = false;
+  const void *kfn = rows ? (const void *)ecs_exact_kernel<NT, DEBUG, row_ok<NT>()>
+                         : (const void *)ecs_exact_kernel<NT, DEBUG, false>;
+#endif
   int occ = 0, cus = 0;
   if (hipError_t e = launch_config(hand ? cfgh : (rows ? cfgr : cfg), kfn, sm, &occ, &cus); e != hipSuccess)
     return e;
@@ -1291,7 +1311,7 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
     rk -= kRows;
   b.rowk = std::max(0L, rk);
   b.rowblk = (int)((b.rowk + (kBlock / kRowW) - 1) / (kBlock / kRowW));
-  if (b.rowblk == 0 || !rows) b.hand = 0; /* hand-off needs rows to take the paths */
+  if (b.rowblk == 0 || !rows || !hand) b.hand = 0; /* hand-off needs rows to take the paths */
   /* continuation launch (hand-off): its blocks, after the main launch */
   b.contblk = (b.hand > 0) ? (int)std::max(1L, std::min((long)a.contblk, slots)) : 0;
   b.begin = a.begin + b.rowk;
@@ -1302,12 +1322,15 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
   if (grid < 0) grid = 0;
   b.nmain = (int)grid;
   if (grid + b.rowblk < 1) return hipSuccess;
+#ifdef PHT_HANDOFF
   if (rows && b.hand > 0) {
     hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG, row_ok<NT>(), true>), dim3((unsigned)(grid + b.rowblk)),
                        dim3(kBlock), sm, st, b);
     if constexpr (row_ok<NT>())
       hipLaunchKernelGGL((ecs_cont_kernel<NT, DEBUG>), dim3((unsigned)b.contblk), dim3(kBlock), sm, st, b);
-  } else if (rows)
+  } else
+#endif
+  if (rows)
     hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG, row_ok<NT>()>), dim3((unsigned)(grid + b.rowblk)), dim3(kBlock), sm,
                        st, b);
   else

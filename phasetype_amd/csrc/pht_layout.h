@@ -98,6 +98,13 @@ constexpr int kXObs = 0;       /* observations processed: must equal the shard's
 constexpr int kXFlagged = 2;   /* observations that hit a cap or guard */
 constexpr int kXUnifCap = 6;   /* UNIF observations past the Poisson table / lam cap: the sweep is an error */
 constexpr int kXOverflow = 15; /* fixed-point z accumulators crossed 2^63 (never in PHT_STAMPS builds) */
+/* DEBUG (per-observation) instantiations of the ECS exact kernels only, not
+ * in PHT_STAMPS builds: lane-rounds (row-rounds on 16-lane rows) that ran the
+ * general ARMS code (an envelope past the converged round's points), and of
+ * those the rounds whose envelope reached past the LDS / row points into
+ * private memory -- the parity tests assert that they exercised that path */
+constexpr int kXDbgGeneral = 8;
+constexpr int kXDbgPrivate = 9;
 PHT_LHD int stats_len(int n) { return 2 * n + n * n + kStatExtra; }
 
 }  // namespace pht

@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(kResThreads) resident_update_kernel(ResidentAr
       if (r.expect >= 0 && (long long)xw[kXObs] != r.expect) atomicOr(r.err, 1);
       if (xw[kXOverflow] != 0ull) atomicOr(r.err, 2);
       if (xw[kXFlagged] != 0ull) atomicAdd(r.flagged, xw[kXFlagged]);
-      if (xw[kXUnifCap] != 0ull) atomicOr(r.err, 16);
+      if (r.unif && xw[kXUnifCap] != 0ull) atomicOr(r.err, 16); /* (word 6 is a DIAG counter in other samplers' diagnostic builds) */
     }
     for (int k = tid; k < m; k += blockDim.x) {
       long long nsum = 0;

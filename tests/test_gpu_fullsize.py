@@ -7,6 +7,9 @@ src/Simulate_AbsCTMC_eq_Aslett_ECS.c:461-479,
 src/Simulate_AbsCTMC_eq_Bladt_MHRS.c:63-114,
 src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:92-147) on the same (S, s, y):
 
+* cfg2: BD-exit n = 5, N = 10^4 exact observations, ECS;
+* cfg3: BD-exit n = 20, N = 10^5 exact observations, ECS (the n = 20 kernels:
+  rows for the longest paths, a 13-point LDS envelope);
 * cfg4: BD-exit n = 10, N = 10^6 exact observations, ECS (bench.py's data);
 * cfg5: BD-exit n = 15, N = 5*10^5, 30 % censored; MHRS, DCS and ECS.
 
@@ -34,6 +37,8 @@ pytestmark = pytest.mark.gpu
 
 # name -> (n, N, censored fraction, method)
 CASES = {
+    "cfg2_ecs": (5, 10_000, 0.0, 2),
+    "cfg3_ecs": (20, 100_000, 0.0, 2),
     "cfg4_ecs": (10, 1_000_000, 0.0, 2),
     "cfg5_mhrs": (15, 500_000, 0.3, 1),
     "cfg5_dcs": (15, 500_000, 0.3, 4),

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--sweeps", type=int, default=8)
     ap.add_argument("--shards", type=int, default=0)
     ap.add_argument("--N", type=int, default=1_000_000)
+    ap.add_argument("--data", type=int, default=1_000_000, help="size of the bench data set the Ns specs index")
     a = ap.parse_args()
     if a.shards:
         return shards(a)
@@ -49,7 +50,7 @@ def main():
     S, s = bd_exit(n)
     T, theta = bd_exit_structure(n)
     nu, zeta = 1 + 50 * theta, np.full(len(theta), 50.0)
-    y, cen = simulate_ph(S, s, 1_000_000, seed=DATA_KEY, censor_frac=0.0)
+    y, cen = simulate_ph(S, s, a.data, seed=DATA_KEY, censor_frac=0.0)
     zexp = P.zexp_for(y)
     Cm = np.ones(T.shape)
     for spec in a.Ns:
