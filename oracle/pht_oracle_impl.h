@@ -743,6 +743,9 @@ typedef struct {
   const orc_sp *sp;
   int j;
   double tnow, y;
+#if ORC_DEV
+  double xr; /* dev (r05): the remaining time y - t as the GPU carries it (xr <- xr - d) */
+#endif
 } ORC_FN(cj_ctx);
 
 #if !ORC_DEV
@@ -763,8 +766,8 @@ static double ORC_FN(cj_dens)(double d, void *vctx) {
   ORC_FN(cj_ctx) *c = (ORC_FN(cj_ctx) *)vctx;
   const orc_sp *sp = c->sp;
   const int n = sp->n, j = c->j;
-  double x1 = c->y - c->tnow - d, r1;
 #if ORC_DEV
+  double x1 = c->xr - d, r1; /* device spec v2 (pht_device.h CjDens) */
   if (x1 > 0) {
     double acc = 0.0;
     for (int i = 0; i < n; i++) acc = fma(sp->V[j + i * n], ORC_EXP_NEG(sp->evals[i] * x1), acc);
@@ -774,6 +777,7 @@ static double ORC_FN(cj_dens)(double d, void *vctx) {
   }
   return ORC_LOG(r1) + ((-d / sp->scale[j]) - sp->logscale[j]);
 #else
+  double x1 = c->y - c->tnow - d, r1;
   double pi1[ORC_MAXN];
   for (int i = 0; i < n; i++) pi1[i] = sp->P[j + i * n];
   if (x1 > 0) r1 = ORC_FN(phtcdf)(sp, x1, pi1); else r1 = 1;
@@ -781,22 +785,71 @@ static double ORC_FN(cj_dens)(double d, void *vctx) {
 #endif
 }
 
-/* LJMA_condjump_r_ars (:184-260) */
-static double ORC_FN(condjump)(const orc_sp *sp, double tnow, int jnow, double y, ORC_FN(rng) *rng,
+#if ORC_DEV
+/* the four starting points of a censored sojourn at once (device spec v2,
+ * pht_device.h CjDens::init4): under pht_ecs_init_ok one vector F at 2b,
+ * F F at b, e^{lambda xr} taylor(-lambda a) at a, taylor(lambda x3) at
+ * xr - a; each sum a sequential fma chain over i */
+static void ORC_FN(cj_init4)(const double xinit[4], double yv[4], void *vctx) {
+  ORC_FN(cj_ctx) *c = (ORC_FN(cj_ctx) *)vctx;
+  const orc_sp *sp = c->sp;
+  const int n = sp->n, j = c->j;
+  const double xr = c->xr, x3 = xr - xinit[3];
+  double lammax = 0.0;
+  for (int i = 0; i < n; i++) lammax = fmax(lammax, fabs(sp->evals[i]));
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  if (pht_ecs_init_ok(lammax, xinit[0], x3)) {
+    for (int i = 0; i < n; i++) {
+      const double F = ORC_EXP_NEG(sp->evals[i] * (xr - xinit[2]));
+      const double v = sp->V[j + i * n];
+      const double Ex = ORC_EXP_NEG(sp->evals[i] * xr);
+      acc[2] = fma(v, F, acc[2]);
+      acc[1] = fma(v, F * F, acc[1]);
+      acc[0] = fma(v, Ex * pht_exp_taylor(-sp->evals[i] * xinit[0]), acc[0]);
+      acc[3] = fma(v, pht_exp_taylor(sp->evals[i] * x3), acc[3]);
+    }
+  } else {
+    for (int k = 0; k < 4; k++) {
+      const double x1 = xr - xinit[k];
+      for (int i = 0; i < n; i++) acc[k] = fma(sp->V[j + i * n], ORC_EXP_NEG(sp->evals[i] * x1), acc[k]);
+    }
+  }
+  for (int k = 0; k < 4; k++) yv[k] = ORC_LOG(acc[k]) + ((-xinit[k] / sp->scale[j]) - sp->logscale[j]);
+}
+#endif
+
+/* LJMA_condjump_r_ars (:184-260); dev: xr = the carried remaining time
+ * (device spec v2), the reference's y - tnow otherwise */
+static double ORC_FN(condjump)(const orc_sp *sp, double tnow, int jnow, double y, double xr, ORC_FN(rng) *rng,
                                int *neval, int *flags) {
   const int n = sp->n;
-  if (tnow >= y) return ORC_FN(rexp)(rng, 1.0 / -sp->S[jnow + jnow * n]);
-  double x = y - tnow, denom;
 #if ORC_DEV
+  if (!(xr > 0)) return ORC_FN(rexp)(rng, 1.0 / -sp->S[jnow + jnow * n]);
+  const double x = xr;
+  double denom;
   double acc = 0.0;
   for (int i = 0; i < n; i++) acc = fma(sp->QQ1[jnow + i * n], ORC_EXP_NEG(sp->evals[i] * x), acc);
   denom = acc;
+  if (ORC_FN(runif)(rng, 0.0, 1.0) < ORC_EXP_NEG(sp->S[jnow + jnow * n] * x) / denom)
+    return x + ORC_FN(rexp)(rng, 1.0 / -sp->S[jnow + jnow * n]);
+  ORC_FN(cj_ctx) ctx = {sp, jnow, tnow, y, x};
+  double xinit[4];
+  xinit[0] = (x) / 1e6;
+  xinit[1] = (x) / 3.0;
+  xinit[2] = xinit[1] * 2.0;
+  xinit[3] = x - xinit[0];
+  double xsamp = 0.0;
+  int ainfo = ORC_FN(arms)(xinit, 0.0, x, ORC_FN(cj_dens), &ctx, 0.0, &xsamp, rng, neval, ORC_FN(cj_init4));
+  if (ainfo) *flags |= (ainfo == 4) ? 4 : 32;
+  return xsamp;
 #else
+  (void)xr;
+  if (tnow >= y) return ORC_FN(rexp)(rng, 1.0 / -sp->S[jnow + jnow * n]);
+  double x = y - tnow, denom;
   double pi[ORC_MAXN];
   for (int i = 0; i < n; i++) pi[i] = 0.0;
   pi[jnow] = 1.0;
   denom = ORC_FN(phtcdf)(sp, x, pi);
-#endif
   if (tnow < y && ORC_FN(runif)(rng, 0.0, 1.0) < ORC_EXP_NEG(sp->S[jnow + jnow * n] * (y - tnow)) / denom)
     return y - tnow + ORC_FN(rexp)(rng, 1.0 / -sp->S[jnow + jnow * n]);
   ORC_FN(cj_ctx) ctx = {sp, jnow, tnow, y};
@@ -809,6 +862,7 @@ static double ORC_FN(condjump)(const orc_sp *sp, double tnow, int jnow, double y
   int ainfo = ORC_FN(arms)(xinit, 0.0, y - tnow, ORC_FN(cj_dens), &ctx, 0.0, &xsamp, rng, neval, NULL);
   if (ainfo) *flags |= (ainfo == 4) ? 4 : 32;
   return xsamp;
+#endif
 }
 
 /* LJMA_samplechain, reverse=0 (:299-418) */
@@ -821,17 +875,33 @@ static void ORC_FN(obs_censored)(const orc_sp *sp, double y, int cens, ORC_FN(rn
   o->B = B;
   double t = 0.0, lastt = 0.0;
   int j = B, lastj = 0, njump = 0;
-  while (t < y || cens) {
+#if ORC_DEV
+  /* device spec v2 (pht_device.h censored_jump): the remaining time carried,
+   * xr <- xr - d; "t < y" decisions read xr > 0 */
+  double xr = y;
+#define ORC_CENS_BEFORE_Y (xr > 0)
+#else
+  double xr = 0.0;
+#define ORC_CENS_BEFORE_Y (t < y)
+#endif
+  while (ORC_CENS_BEFORE_Y || cens) {
 #if ORC_DEV
     if (njump++ >= ORC_MAX_JUMPS) { o->flags |= 8; break; }
 #endif
     lastt = t;
     lastj = j;
-    double d = ORC_FN(condjump)(sp, t, j, y, rng, neval, &o->flags);
+    double d = ORC_FN(condjump)(sp, t, j, y, xr, rng, neval, &o->flags);
     t += d;
+#if ORC_DEV
+    xr = xr - d;
+#endif
     target = ORC_FN(u)(rng);
-    if (t < y) {
+    if (ORC_CENS_BEFORE_Y) {
+#if ORC_DEV
+      double x1 = xr;
+#else
       double x1 = y - t;
+#endif
 #if ORC_DEV
       double E[ORC_MAXN], w[ORC_MAXN], r2 = 0.0;
       (void)sofar;
@@ -876,11 +946,12 @@ static void ORC_FN(obs_censored)(const orc_sp *sp, double y, int cens, ORC_FN(rn
 #endif
     }
     if (j == n) break;
-    if (t < y || cens) {
+    if (ORC_CENS_BEFORE_Y || cens) {
       ORC_FN(zadd)(o, lastj, t - lastt, zscale);
       o->N[lastj + j * n]++;
     }
   }
+#undef ORC_CENS_BEFORE_Y
   if (cens == 0) ORC_FN(zadd)(o, lastj, y - lastt, zscale);
   else ORC_FN(zadd)(o, lastj, t - lastt, zscale);
   o->pre = lastj;

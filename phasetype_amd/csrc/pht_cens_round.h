@@ -79,7 +79,7 @@ __device__ __forceinline__ void cens_round_body(const SweepArgs &a, unsigned blk
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr};
   Lane ln;
   ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
-  CensLane cl;
+  CensLane<NT> cl;
   using EnvL = EnvLdsXY<(cens_env_lds<NT>() ? cens_env_k<NT>() : 1), kBlock>;
   typename std::conditional<cens_env_lds<NT>(), EnvL, EnvPrivate>::type env;
   double spill[2 * EnvL::kSpill];

@@ -850,56 +850,115 @@ __device__ __forceinline__ void ecs_exact(const Par<NT> &P, double y, Lane &ln, 
 }
 
 /* ===================================================== censored path */
+/*
+ * Device specification of the censored path (r05, "v2"; the oracle's dev
+ * variant orcD_obs_censored follows it operation for operation):
+ *  - the remaining time to y is carried, xr <- xr - d (the reference
+ *    recomputes y - t); every "t < y" decision reads xr > 0 and the sojourn
+ *    density's argument is xr - d (the exact path's y_t carry, r01);
+ *  - the four ARMS starting points share one exponential vector under
+ *    pht_ecs_init_ok, as the exact path's (pht_detmath.h): F at 2b directly,
+ *    F F at b, e^{lambda xr} taylor(-lambda a) at a, taylor(lambda x3) at
+ *    xr - a; outside that condition the four vectors directly.
+ * With the carry, the exponentials e^{lambda_i xr} of a jump's stay test
+ * (denominator), of ARMS's xprev = 0 and of the previous jump's categorical
+ * are the same values, and so are those of the accepted proposal and the
+ * next categorical: the GPU computes each vector once (bit-identical to
+ * recomputing it).  The statistics keep the absolute times (z += t - lastt).
+ */
 template <int NT>
-struct CjDens { /* log F_{P_j}(y - t - d) + log dexp(d; 1/-S_jj) */
-  static constexpr bool kInit4 = false;
-  __device__ __forceinline__ void init4(const double *, double *) {}
+struct CjDens { /* log F_{P_j}(xr - d) + log dexp(d; 1/-S_jj) */
+  static constexpr bool kInit4 = true;
   const Par<NT> &P;
   int j;
-  double tnow, y, scale, logscale;
-  __device__ __forceinline__ double operator()(double d) const {
+  double xr, scale, logscale;
+  const double *Ex; /* e^{lambda_i xr}: the density at d = 0 */
+  double lammax;
+  double lastd;
+  double Elast[PHT_VEC(NT)]; /* the vector of the most recent evaluation at lastd != 0 */
+  __device__ __forceinline__ double operator()(double d) {
     const int n = P.n();
-    const double x1 = y - tnow - d;
+    const double x1 = xr - d;
     double r1;
     if (x1 > 0) {
       double acc = 0.0;
+      if (d == 0.0) {
 #pragma unroll
-      for (int i = 0; i < n; i++) acc = fma(P.V(j, i), pht_exp_neg(P.evals(i) * x1), acc);
+        for (int i = 0; i < n; i++) acc = fma(P.V(j, i), Ex[i], acc);
+      } else {
+#pragma unroll
+        for (int i = 0; i < n; i++) Elast[i] = pht_exp_neg(P.evals(i) * x1);
+#pragma unroll
+        for (int i = 0; i < n; i++) acc = fma(P.V(j, i), Elast[i], acc);
+        lastd = d;
+      }
       r1 = acc;
     } else {
       r1 = 1;
     }
     return pht_log(r1) + ((-d / scale) - logscale);
   }
+  /* the four starting points at once (xinit = {a, b, 2b, xr - a}; the
+   * caller has checked 0 < a < b < 2b < xr - a < xr, so every x1 > 0) */
+  __device__ __forceinline__ void init4(const double xinit[4], double yv[4]) {
+    const int n = P.n();
+    const double x3 = xr - xinit[3];
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (pht_ecs_init_ok(lammax, xinit[0], x3)) {
+#pragma unroll
+      for (int i = 0; i < n; i++) {
+        const double F = pht_exp_neg(P.evals(i) * (xr - xinit[2]));
+        const double v = P.V(j, i);
+        acc[2] = fma(v, F, acc[2]);
+        acc[1] = fma(v, F * F, acc[1]);
+        acc[0] = fma(v, Ex[i] * pht_exp_taylor(-P.evals(i) * xinit[0]), acc[0]);
+        acc[3] = fma(v, pht_exp_taylor(P.evals(i) * x3), acc[3]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const double x1 = xr - xinit[k];
+#pragma unroll
+        for (int i = 0; i < n; i++) acc[k] = fma(P.V(j, i), pht_exp_neg(P.evals(i) * x1), acc[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) yv[k] = pht_log(acc[k]) + ((-xinit[k] / scale) - logscale);
+  }
 };
 
 /* path state of a censored observation between jumps */
+template <int NT>
 struct CensLane {
   double y, t, lastt;
+  double xr;                /* remaining time to y, carried xr <- xr - d (device spec v2) */
   int j, lastj, njump;
+  bool haveEx;              /* Ex = e^{lambda_i xr} (from the previous jump's categorical) */
+  double Ex[PHT_VEC(NT)];
 };
 
 /* start state (LJMA_samplechain, src/Simulate_AbsCTMC_gt_Aslett_DCS.c:315) */
 template <int NT, class Sink>
-__device__ __forceinline__ void censored_begin(const Par<NT> &P, double y, Lane &ln, Sink &sk, CensLane &c) {
+__device__ __forceinline__ void censored_begin(const Par<NT> &P, double y, Lane &ln, Sink &sk, CensLane<NT> &c) {
   const double target = dev_u(ln.r);
   const int B = pistart(P, target, ln.flags);
   sk.start(B);
   c.y = y;
   c.t = 0.0;
   c.lastt = 0.0;
+  c.xr = y;
   c.j = B;
   c.lastj = 0;
   c.njump = 0;
+  c.haveEx = false;
 }
 
 /* one jump of the censored path (the loop body of LJMA_samplechain,
  * src/Simulate_AbsCTMC_gt_Aslett_DCS.c:320-388, with LJMA_condjump_r_ars
  * :184-260); true = the path is complete and recorded */
 template <int NT, class Env, class Sink>
-__device__ __forceinline__ bool censored_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, CensLane &c) {
+__device__ __forceinline__ bool censored_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, CensLane<NT> &c) {
   const int n = P.n();
-  const double y = c.y;
   bool done = false;
   if (c.njump++ >= kMaxJumps) {
     ln.flags |= kFlagJumpCap;
@@ -910,43 +969,59 @@ __device__ __forceinline__ bool censored_jump(const Par<NT> &P, Lane &ln, Env &e
     c.lastt = t;
     c.lastj = j;
     const double Sjj = P.S(j, j);
+    const double x = c.xr;
     double d;
+    CjDens<NT> f{P, j, x, P.scale(j), P.logscale(j), c.Ex, 0.0, -1.0, {}};
+    bool armsd = false; /* d from ARMS: its vectors may serve the categorical */
     /* LJMA_condjump_r_ars */
-    if (t >= y) {
+    if (!(x > 0)) { /* t >= y */
       d = dev_rexp(ln.r, 1.0 / -Sjj);
     } else {
-      const double x = y - t;
+      if (!c.haveEx) {
+#pragma unroll
+        for (int i = 0; i < n; i++) c.Ex[i] = pht_exp_neg(P.evals(i) * x);
+      }
       double denom = 0.0;
 #pragma unroll
-      for (int i = 0; i < n; i++) denom = fma(P.QQ1(j, i), pht_exp_neg(P.evals(i) * x), denom);
-      if (t < y && dev_runif(ln.r, 0.0, 1.0) < pht_exp_neg(Sjj * (y - t)) / denom) {
-        d = y - t + dev_rexp(ln.r, 1.0 / -Sjj);
+      for (int i = 0; i < n; i++) denom = fma(P.QQ1(j, i), c.Ex[i], denom);
+      if (dev_runif(ln.r, 0.0, 1.0) < pht_exp_neg(Sjj * x) / denom) {
+        d = x + dev_rexp(ln.r, 1.0 / -Sjj);
       } else {
-        CjDens<NT> f{P, j, t, y, P.scale(j), P.logscale(j)};
+        f.lammax = lam_max(P);
         double xinit[4];
-        xinit[0] = (y - t) / 1e6;
-        xinit[1] = (y - t) / 3.0;
+        xinit[0] = (x) / 1e6;
+        xinit[1] = (x) / 3.0;
         xinit[2] = xinit[1] * 2.0;
-        xinit[3] = y - t - xinit[0];
+        xinit[3] = x - xinit[0];
         double xsamp = 0.0;
-        const int ainfo = arms(env, xinit, 0.0, y - t, f, 0.0, xsamp, ln);
+        const int ainfo = arms(env, xinit, 0.0, x, f, 0.0, xsamp, ln);
         if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
         d = xsamp;
+        armsd = true;
       }
     }
     const int lastj = j;
     const double tn = t + d;
     c.t = tn;
+    const double x1 = x - d;
+    c.xr = x1;
+    c.haveEx = false;
     const double target = dev_u(ln.r);
     int nj;
-    if (tn < y) {
-      const double x1 = y - tn;
-      double E[PHT_VEC(NT)];
+    if (x1 > 0) { /* tn < y: x1 > 0 needs x > 0 and d < x, i.e. the ARMS branch */
+      /* e^{lambda_i x1}: the accepted proposal's (d == lastd) or, for d = 0,
+       * the stay test's vector; they become the next jump's Ex */
+      if (armsd && d == f.lastd) {
 #pragma unroll
-      for (int i = 0; i < n; i++) E[i] = pht_exp_neg(P.evals(i) * x1);
+        for (int i = 0; i < n; i++) c.Ex[i] = f.Elast[i];
+      } else if (!(d == 0.0)) {
+#pragma unroll
+        for (int i = 0; i < n; i++) c.Ex[i] = pht_exp_neg(P.evals(i) * x1);
+      }
+      c.haveEx = true;
       double r2 = 0.0;
 #pragma unroll
-      for (int i = 0; i < n; i++) r2 = fma(P.V(lastj, i), E[i], r2);
+      for (int i = 0; i < n; i++) r2 = fma(P.V(lastj, i), c.Ex[i], r2);
       const int cnt = P.nsuccP(lastj);
       const double tg = target * r2;
       double sofar = 0.0;
@@ -955,7 +1030,7 @@ __device__ __forceinline__ bool censored_jump(const Par<NT> &P, Lane &ln, Env &e
         const int k = P.succP(lastj, q);
         double r1 = 0.0;
 #pragma unroll
-        for (int i = 0; i < n; i++) r1 = fma(P.QQ1(k, i), E[i], r1);
+        for (int i = 0; i < n; i++) r1 = fma(P.QQ1(k, i), c.Ex[i], r1);
         sofar += r1 * P.P(lastj, k);
         if (!(sofar < tg)) {
           sel = k;
@@ -1004,7 +1079,7 @@ __device__ __forceinline__ bool censored_jump(const Par<NT> &P, Lane &ln, Env &e
 
 template <int NT, class Env, class Sink>
 __device__ __forceinline__ void censored(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
-  CensLane c;
+  CensLane<NT> c;
   censored_begin(P, y, ln, sk, c);
   while (!censored_jump(P, ln, env, sk, c)) {
   }
