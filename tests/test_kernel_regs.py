@@ -36,6 +36,20 @@ def test_ecs_two_waves_no_spill(regs, nt, kind):
     assert d["vgpr_spill"] == 0, (name, d)
 
 
+@pytest.mark.parametrize("kind,ceiling", [("ecs_exact_kernelILi20ELb0ELb0ELb0E", 43),
+                                          ("ecs_exact_kernelILi20ELb0ELb1ELb0E", 130),
+                                          ("ecs_chains_kernelILi20EE", 43)])
+def test_ecs_n20_spill_ceiling(regs, kind, ceiling):
+    """n = 20 runs two waves per SIMD with some VGPRs spilled (faster than one
+    wave without spills: cfg3 kernel 0.812 vs 0.865 ms, profiles/r05/cfg3/
+    w1_ab_*.jsonl); the r04 counts are the ceiling, so the spills cannot grow
+    unnoticed."""
+    hits = {k: v for k, v in regs.items() if kind in k}
+    assert len(hits) == 1, (kind, list(hits))
+    (name, d), = hits.items()
+    assert d["waves_per_simd"] >= 2 and d["vgpr_spill"] <= ceiling, (name, d)
+
+
 @pytest.mark.parametrize("nt", [3, 5, 10, 15])
 def test_ecs_handoff_instantiation(regs, nt):
     """The hand-off kernel (its own instantiation, launched only in the
