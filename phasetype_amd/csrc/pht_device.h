@@ -953,153 +953,128 @@ __device__ __forceinline__ void censored_begin(const Par<NT> &P, double y, Lane 
   c.haveEx = false;
 }
 
-/* The first part of one jump of the censored path (the loop body of
- * LJMA_samplechain, src/Simulate_AbsCTMC_gt_Aslett_DCS.c:320-388, and
- * LJMA_condjump_r_ars :184-260 up to its ARMS call).  Returns
- *   0: the sojourn d is drawn (t >= y: exponential; or the stay-past-y
- *      branch) and censored_finish is next;
- *   1: the sojourn needs ARMS on (0, xr) with the CjDens of (j, xr);
- *   2: the path is complete (jump cap) and recorded. */
-template <int NT, class Sink>
-__device__ __forceinline__ int censored_step(const Par<NT> &P, Lane &ln, Sink &sk, CensLane<NT> &c, double &d) {
-  const int n = P.n();
-  if (c.njump++ >= kMaxJumps) {
-    ln.flags |= kFlagJumpCap;
-    sk.z(c.lastj, c.t - c.lastt);
-    sk.pre(c.lastj);
-    sk.N(c.lastj, c.lastj);
-    return 2;
-  }
-  const int j = c.j;
-  c.lastt = c.t;
-  c.lastj = j;
-  const double Sjj = P.S(j, j);
-  const double x = c.xr;
-  if (!(x > 0)) { /* t >= y */
-    d = dev_rexp(ln.r, 1.0 / -Sjj);
-    return 0;
-  }
-  if (!c.haveEx) {
-#pragma unroll
-    for (int i = 0; i < n; i++) c.Ex[i] = pht_exp_neg(P.evals(i) * x);
-    c.haveEx = true;
-  }
-  double denom = 0.0;
-#pragma unroll
-  for (int i = 0; i < n; i++) denom = fma(P.QQ1(j, i), c.Ex[i], denom);
-  if (dev_runif(ln.r, 0.0, 1.0) < pht_exp_neg(Sjj * x) / denom) {
-    d = x + dev_rexp(ln.r, 1.0 / -Sjj);
-    return 0;
-  }
-  return 1;
-}
-
-/* the sojourn density of the jump censored_step asked ARMS for */
-template <int NT>
-__device__ __forceinline__ CjDens<NT> censored_dens(const Par<NT> &P, const CensLane<NT> &c, double lam) {
-  return CjDens<NT>{P, c.j, c.xr, P.scale(c.j), P.logscale(c.j), c.Ex, lam, -1.0, {}};
-}
-
-/* The rest of the jump once d is drawn: the next state (:345-386) and the
- * statistics; f = the ARMS density of the jump (its last evaluation's
- * vector serves the categorical when d is that point) or nullptr.  Returns
- * true when the path is complete and recorded. */
-template <int NT, class Sink>
-__device__ __forceinline__ bool censored_finish(const Par<NT> &P, Lane &ln, Sink &sk, CensLane<NT> &c, double d,
-                                                const CjDens<NT> *f) {
-  const int n = P.n();
-  const int lastj = c.lastj;
-  const double x = c.xr;
-  const double tn = c.t + d;
-  c.t = tn;
-  const double x1 = x - d;
-  c.xr = x1;
-  const double target = dev_u(ln.r);
-  int nj;
-  if (x1 > 0) { /* tn < y: x1 > 0 needs x > 0 and d < x, i.e. the ARMS branch */
-    /* e^{lambda_i x1}: the accepted proposal's (d == lastd) or, for d = 0,
-     * the stay test's vector (c.Ex); they become the next jump's Ex */
-    if (f && d == f->lastd) {
-#pragma unroll
-      for (int i = 0; i < n; i++) c.Ex[i] = f->Elast[i];
-    } else if (!(d == 0.0)) {
-#pragma unroll
-      for (int i = 0; i < n; i++) c.Ex[i] = pht_exp_neg(P.evals(i) * x1);
-    }
-    c.haveEx = true;
-    double r2 = 0.0;
-#pragma unroll
-    for (int i = 0; i < n; i++) r2 = fma(P.V(lastj, i), c.Ex[i], r2);
-    const int cnt = P.nsuccP(lastj);
-    const double tg = target * r2;
-    double sofar = 0.0;
-    int q = 0, sel = -1;
-    for (; q < cnt; q++) {
-      const int k = P.succP(lastj, q);
-      double r1 = 0.0;
-#pragma unroll
-      for (int i = 0; i < n; i++) r1 = fma(P.QQ1(k, i), c.Ex[i], r1);
-      sofar += r1 * P.P(lastj, k);
-      if (!(sofar < tg)) {
-        sel = k;
-        break;
-      }
-    }
-    if (sel < 0) {
-      ln.flags |= kFlagScanEnd;
-      sel = (cnt > 0) ? P.succP(lastj, cnt - 1) : 0;
-    }
-    nj = sel;
-  } else {
-    c.haveEx = false;
-    const int cnt = P.nsuccPf(lastj);
-    double sofar = 0.0;
-    int sel = -1;
-    for (int q = 0; q < cnt; q++) {
-      const int k = P.succPf(lastj, q);
-      sofar += P.Pf(lastj, k);
-      if (!(sofar < target)) {
-        sel = k;
-        break;
-      }
-    }
-    if (sel < 0) {
-      ln.flags |= kFlagScanEnd;
-      sel = (cnt > 0) ? P.succPf(lastj, cnt - 1) : 0;
-    }
-    nj = sel;
-  }
-  c.j = nj;
-  if (nj == n) {
-    sk.z(c.lastj, c.t - c.lastt);
-    sk.pre(c.lastj);
-    sk.N(c.lastj, c.lastj);
-    return true;
-  }
-  sk.z(lastj, tn - c.lastt);
-  sk.N(lastj, nj);
-  ln.njump++;
-  return false;
-}
-
-/* one whole jump (ARMS inline); true = the path is complete and recorded */
+/* one jump of the censored path (the loop body of LJMA_samplechain,
+ * src/Simulate_AbsCTMC_gt_Aslett_DCS.c:320-388, with LJMA_condjump_r_ars
+ * :184-260); true = the path is complete and recorded */
 template <int NT, class Env, class Sink>
 __device__ __forceinline__ bool censored_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, CensLane<NT> &c) {
-  double d = 0.0;
-  const int st = censored_step(P, ln, sk, c, d);
-  if (st == 2) return true;
-  if (st == 0) return censored_finish(P, ln, sk, c, d, (const CjDens<NT> *)nullptr);
-  CjDens<NT> f = censored_dens(P, c, lam_max(P));
-  const double x = c.xr;
-  double xinit[4];
-  xinit[0] = (x) / 1e6;
-  xinit[1] = (x) / 3.0;
-  xinit[2] = xinit[1] * 2.0;
-  xinit[3] = x - xinit[0];
-  double xsamp = 0.0;
-  const int ainfo = arms(env, xinit, 0.0, x, f, 0.0, xsamp, ln);
-  if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
-  return censored_finish(P, ln, sk, c, xsamp, &f);
+  const int n = P.n();
+  bool done = false;
+  if (c.njump++ >= kMaxJumps) {
+    ln.flags |= kFlagJumpCap;
+    done = true;
+  } else {
+    const double t = c.t;
+    const int j = c.j;
+    c.lastt = t;
+    c.lastj = j;
+    const double Sjj = P.S(j, j);
+    const double x = c.xr;
+    double d;
+    CjDens<NT> f{P, j, x, P.scale(j), P.logscale(j), c.Ex, 0.0, -1.0, {}};
+    bool armsd = false; /* d from ARMS: its vectors may serve the categorical */
+    /* LJMA_condjump_r_ars */
+    if (!(x > 0)) { /* t >= y */
+      d = dev_rexp(ln.r, 1.0 / -Sjj);
+    } else {
+      if (!c.haveEx) {
+#pragma unroll
+        for (int i = 0; i < n; i++) c.Ex[i] = pht_exp_neg(P.evals(i) * x);
+      }
+      double denom = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) denom = fma(P.QQ1(j, i), c.Ex[i], denom);
+      if (dev_runif(ln.r, 0.0, 1.0) < pht_exp_neg(Sjj * x) / denom) {
+        d = x + dev_rexp(ln.r, 1.0 / -Sjj);
+      } else {
+        f.lammax = lam_max(P);
+        double xinit[4];
+        xinit[0] = (x) / 1e6;
+        xinit[1] = (x) / 3.0;
+        xinit[2] = xinit[1] * 2.0;
+        xinit[3] = x - xinit[0];
+        double xsamp = 0.0;
+        const int ainfo = arms(env, xinit, 0.0, x, f, 0.0, xsamp, ln);
+        if (ainfo) ln.flags |= (ainfo == 4) ? kFlagArmsCap : kFlagArmsErr;
+        d = xsamp;
+        armsd = true;
+      }
+    }
+    const int lastj = j;
+    const double tn = t + d;
+    c.t = tn;
+    const double x1 = x - d;
+    c.xr = x1;
+    c.haveEx = false;
+    const double target = dev_u(ln.r);
+    int nj;
+    if (x1 > 0) { /* tn < y: x1 > 0 needs x > 0 and d < x, i.e. the ARMS branch */
+      /* e^{lambda_i x1}: the accepted proposal's (d == lastd) or, for d = 0,
+       * the stay test's vector; they become the next jump's Ex */
+      if (armsd && d == f.lastd) {
+#pragma unroll
+        for (int i = 0; i < n; i++) c.Ex[i] = f.Elast[i];
+      } else if (!(d == 0.0)) {
+#pragma unroll
+        for (int i = 0; i < n; i++) c.Ex[i] = pht_exp_neg(P.evals(i) * x1);
+      }
+      c.haveEx = true;
+      double r2 = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) r2 = fma(P.V(lastj, i), c.Ex[i], r2);
+      const int cnt = P.nsuccP(lastj);
+      const double tg = target * r2;
+      double sofar = 0.0;
+      int q = 0, sel = -1;
+      for (; q < cnt; q++) {
+        const int k = P.succP(lastj, q);
+        double r1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < n; i++) r1 = fma(P.QQ1(k, i), c.Ex[i], r1);
+        sofar += r1 * P.P(lastj, k);
+        if (!(sofar < tg)) {
+          sel = k;
+          break;
+        }
+      }
+      if (sel < 0) {
+        ln.flags |= kFlagScanEnd;
+        sel = (cnt > 0) ? P.succP(lastj, cnt - 1) : 0;
+      }
+      nj = sel;
+    } else {
+      const int cnt = P.nsuccPf(lastj);
+      double sofar = 0.0;
+      int sel = -1;
+      for (int q = 0; q < cnt; q++) {
+        const int k = P.succPf(lastj, q);
+        sofar += P.Pf(lastj, k);
+        if (!(sofar < target)) {
+          sel = k;
+          break;
+        }
+      }
+      if (sel < 0) {
+        ln.flags |= kFlagScanEnd;
+        sel = (cnt > 0) ? P.succPf(lastj, cnt - 1) : 0;
+      }
+      nj = sel;
+    }
+    c.j = nj;
+    if (nj == n) {
+      done = true;
+    } else {
+      sk.z(lastj, tn - c.lastt);
+      sk.N(lastj, nj);
+      ln.njump++;
+    }
+  }
+  if (done) {
+    sk.z(c.lastj, c.t - c.lastt);
+    sk.pre(c.lastj);
+    sk.N(c.lastj, c.lastj);
+  }
+  return done;
 }
 
 template <int NT, class Env, class Sink>

@@ -81,43 +81,5 @@ struct EnvLdsXY {
   __device__ __forceinline__ void sCUM(int k, double v) { cm[k] = v; }
 };
 
-/* x and y of the first K points in REGISTERS (the ECS latency-mode variant,
- * PHT_ECS_LAT builds; r05 experiment): every access with a
- * compile-time position is a register, a run-time position selects over the
- * K registers (no dynamic indexing, so the arrays never move to scratch);
- * points K..99 and cum in private memory as EnvLdsXY's.  Same results as
- * EnvPrivate for any K. */
-template <int K>
-struct EnvRegXY {
-  static constexpr bool kUnroll = true;
-  static constexpr int kLds = K;
-  static constexpr int kSpill = 100 - K;
-  double xr[K], yr[K];
-  PHT_PRIV double *ov; /* [2][kSpill] x, y beyond K */
-  PHT_PRIV double *cm; /* [100] cum */
-  int cnt;
-  double ymax;
-  __device__ __forceinline__ void bind(PHT_PRIV double *spill, PHT_PRIV double *cum) {
-    ov = spill;
-    cm = cum;
-  }
-  __device__ __forceinline__ static double pick(const double *a, int k) {
-    double v = a[0];
-#pragma unroll
-    for (int i = 1; i < K; i++) v = (k == i) ? a[i] : v;
-    return v;
-  }
-  __device__ __forceinline__ static void put(double *a, int k, double v) {
-#pragma unroll
-    for (int i = 0; i < K; i++) a[i] = (k == i) ? v : a[i];
-  }
-  __device__ __forceinline__ double X(int k) const { if (k < K) return pick(xr, k); return ov[k - K]; }
-  __device__ __forceinline__ double Y(int k) const { if (k < K) return pick(yr, k); return ov[kSpill + k - K]; }
-  __device__ __forceinline__ double CUM(int k) const { return cm[k]; }
-  __device__ __forceinline__ void sX(int k, double v) { if (k < K) put(xr, k, v); else ov[k - K] = v; }
-  __device__ __forceinline__ void sY(int k, double v) { if (k < K) put(yr, k, v); else ov[kSpill + k - K] = v; }
-  __device__ __forceinline__ void sCUM(int k, double v) { cm[k] = v; }
-};
-
 }  // namespace pht
 #endif

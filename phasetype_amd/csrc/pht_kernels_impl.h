@@ -702,7 +702,7 @@ __device__ __forceinline__ void stage_ecs_params(const SweepArgs &a, PHT_LDS uns
 /* blk / nblk: the block's index and the block count of its chain's grid
  * (blockIdx.x / gridDim.x, except in ecs_chains_kernel).  HAND: the launch
  * has row blocks that continue the paths this body hands off (a.hand) */
-template <int NT, bool DEBUG, bool HAND = false, bool LAT = false>
+template <int NT, bool DEBUG, bool HAND = false>
 __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
@@ -729,18 +729,10 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
   /* the envelope's x and y in LDS (lane-interleaved) up to PHT_SLOW_K
    * points; cum lives in registers within a round (pht_ecs_round.h) and in
    * private memory for the general ARMS code */
-  /* (LAT: the latency-mode experiment, PHT_ECS_LAT builds: the converged
-   * round's 13 points in registers, EnvRegXY) */
-  using EnvT = typename std::conditional<LAT, EnvRegXY<kRoundCap>, EnvLdsXY<ecs_env_k<NT>(), kBlock>>::type;
-  EnvT env;
-  double spill[2 * EnvT::kSpill];
+  EnvLdsXY<ecs_env_k<NT>(), kBlock> env;
+  double spill[2 * EnvLdsXY<ecs_env_k<NT>(), kBlock>::kSpill];
   double cumv[100];
-  if constexpr (LAT) {
-    (void)envl;
-    env.bind((PHT_PRIV double *)spill, (PHT_PRIV double *)cumv);
-  } else {
-    env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill, (PHT_PRIV double *)cumv);
-  }
+  env.bind(envl, threadIdx.x, (PHT_PRIV double *)spill, (PHT_PRIV double *)cumv);
   Sink<DEBUG> sk{zq, Bc, Nc, n, a.zscale, nullptr, nullptr, nullptr, nullptr, xc};
   Lane ln;
 #ifdef PHT_STAMPS
@@ -1272,17 +1264,6 @@ ecs_exact_kernel(SweepArgs a) {
   }
 }
 
-#ifdef PHT_ECS_LAT
-/* latency-mode experiment (r05): one wave per SIMD (up
- * to 512 VGPRs), the converged round's envelope in registers; every ECS
- * exact launch of a PHT_ECS_LAT variant build takes it (no rows) */
-template <int NT, bool DEBUG>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
-ecs_lat_kernel(SweepArgs a) {
-  ecs_exact_body<NT, DEBUG, false, true>(a, blockIdx.x, gridDim.x);
-}
-#endif
-
 /* the hand-off's continuation launch: rows take the records the one-lane
  * blocks of the launch before wrote (all complete), until none is left */
 template <int NT, bool DEBUG>
@@ -1318,25 +1299,6 @@ template <int NT, bool DEBUG>
 static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
   static LaunchCfg cfg, cfgr, cfgh;
   const int sm = smem_bytes_ecs<NT>(a.n);
-#ifdef PHT_ECS_LAT
-  {
-    static LaunchCfg cfgl;
-    int occ = 0, cus = 0;
-    if (hipError_t e = launch_config(cfgl, (const void *)ecs_lat_kernel<NT, DEBUG>, sm, &occ, &cus); e != hipSuccess)
-      return e;
-    SweepArgs b = a;
-    b.rowk = 0;
-    b.rowblk = 0;
-    b.hand = 0;
-    long grid = (long)cus * occ;
-    const long want = (a.count + kBlock - 1) / kBlock;
-    if (grid > want) grid = want;
-    if (grid < 1) return hipSuccess;
-    b.nmain = (int)grid;
-    hipLaunchKernelGGL((ecs_lat_kernel<NT, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, b);
-    return hipGetLastError();
-  }
-#endif
   const bool rows = row_ok<NT>() && a.rowk > 0;
 #ifdef PHT_HANDOFF
   const bool hand = rows && a.hand > 0;
