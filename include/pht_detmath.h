@@ -487,6 +487,39 @@ PHT_HD double pht_log(double x) {
   return (x != x || x <= 0.0 || x == INFINITY) ? spec : res;
 }
 
+/* pht_log for a positive normal finite x (2^-1022 <= x < inf): the same
+ * value without the subnormal scaling and the special-case selects (the
+ * sampled uniforms of the exponential draws, [2^-53, 1 - 2^-53]) */
+PHT_HD double pht_log_pos(double x) {
+  const double LN2_HI = 0x1.62e42fee00000p-1;
+  const double LN2_LO = 0x1.a39ef35793c76p-33;
+  const uint64_t u = pht_d2u(x);
+  const int k0 = (int)((u >> 52) & 0x7ff) - 1023;
+  const uint64_t mant = u & 0x000fffffffffffffULL;
+  const int half = (mant >= 0x6a09e667f3bcdULL);
+  const uint64_t zb = mant | (half ? 0x3fe0000000000000ULL : 0x3ff0000000000000ULL);
+  const int k = k0 + half;
+  const int idx = (int)(mant >> 45) + (half ? 128 : 0);
+  const double z = pht_u2d(zb);
+  const double invc = PHT_LOG_TAB[3 * idx], logc = PHT_LOG_TAB[3 * idx + 1], logclo = PHT_LOG_TAB[3 * idx + 2];
+  const double r = fma(z, invc, -1.0);
+  const double kd = (double)k;
+  const double a = kd * LN2_HI;
+  const double w = a + logc;
+  const double werr = (a - w) + logc;
+  const double hi = w + r;
+  const double lo = (w - hi) + r;
+  double q = -0x1.0000000000000p-3;
+  q = fma(q, r, 0x1.2492492492492p-3);
+  q = fma(q, r, -0x1.5555555555555p-3);
+  q = fma(q, r, 0x1.999999999999ap-3);
+  q = fma(q, r, -0x1.0000000000000p-2);
+  q = fma(q, r, 0x1.5555555555555p-2);
+  q = fma(q, r, -0x1.0000000000000p-1);
+  const double tail = fma(r * r, q, (lo + werr) + fma(kd, LN2_LO, logclo));
+  return hi + tail;
+}
+
 /* e^u for |u| <= 2^-8 (degree-5 Taylor, truncation < 2^-60 relative) */
 PHT_HD double pht_exp_taylor(double u) {
   double q = 8.3333333333333332177e-03;      /* 1/5! */

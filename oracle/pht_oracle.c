@@ -702,6 +702,7 @@ void orc_gibbs(int dev, int it, int mhit, int method, int n, int m, const double
 /* primitive probes for tests/test_detmath.py and tests/test_philox.py */
 void orc_detexp_v(const double *x, double *y, long n) { for (long i = 0; i < n; i++) y[i] = pht_exp(x[i]); }
 void orc_detlog_v(const double *x, double *y, long n) { for (long i = 0; i < n; i++) y[i] = pht_log(x[i]); }
+void orc_detlogpos_v(const double *x, double *y, long n) { for (long i = 0; i < n; i++) y[i] = pht_log_pos(x[i]); }
 void orc_philox(const uint32_t *ctr, uint32_t k0, uint32_t k1, uint32_t *out) {
   pht_u32x4 c = {{ctr[0], ctr[1], ctr[2], ctr[3]}};
   pht_u32x4 w = pht_philox4x32_10(c, k0, k1);

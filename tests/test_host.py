@@ -372,3 +372,18 @@ def test_detmath_log_accuracy(orc):
     out = np.zeros_like(sp)
     orc.lib.orc_detlog_v(sp.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p), C.c_long(len(sp)))
     assert np.isnan(out[0]) and np.isnan(out[1]) and out[2] == -np.inf and out[3] == np.inf
+
+
+def test_log_pos_equals_log_on_the_draws_domain(orc):
+    """pht_log_pos (the exponential draws' logarithm, dev_rexp) returns
+    pht_log's value bit for bit on positive normal numbers, in particular on
+    the 53-bit uniforms (2m + 1) 2^-53 it is given (pht_philox.h pht_u01)."""
+    rng = np.random.default_rng(16)
+    m = rng.integers(0, 2 ** 52, 500000, dtype=np.uint64)
+    u = (2.0 * m.astype(np.float64) + 1.0) * 2.0 ** -53
+    x = np.concatenate([u, np.array([2.0 ** -53, 1.0 - 2.0 ** -53, 0.5, 2.0 ** -1022, 1e300, 0.7071067811865476,
+                                     0.7071067811865475]), np.exp(rng.uniform(-700, 700, 100000))])
+    a, b = np.zeros_like(x), np.zeros_like(x)
+    orc.lib.orc_detlog_v(x.ctypes.data_as(C.c_void_p), a.ctypes.data_as(C.c_void_p), C.c_long(len(x)))
+    orc.lib.orc_detlogpos_v(x.ctypes.data_as(C.c_void_p), b.ctypes.data_as(C.c_void_p), C.c_long(len(x)))
+    assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
