@@ -342,7 +342,12 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
       if (!((t < y && j < n) || (cens && j < n))) {
         inatt = false;
         if (!(t < y) && lastj < n && P.s(lastj) > 0.0) {
-          atomicMin(&a.mbest[task], mhrs_pack(att, lastj));
+          /* one lane per task (round 0): the task's only writer, stopping at
+           * its first success, so a plain store is the atomicMin's result
+           * (device-scope atomics go to memory: 48 MB of writes per round-0
+           * launch at cfg4, profiles/r05/mhrs/pmc_cfg4_mhrs_per_kernel.json) */
+          if constexpr (W == 1) a.mbest[task] = mhrs_pack(att, lastj);
+          else atomicMin(&a.mbest[task], mhrs_pack(att, lastj));
           have = false; /* this lane's further attempts are larger */
         }
       }

@@ -20,7 +20,7 @@ run cfg5_mhrs --n 15 --N 500000 --censor 0.3 --method MHRS --steps 100
 run cfg4_mhrs_steady --n 10 --N 1000000 --method MHRS --warmup 200 --steps 100
 run cfg5_mhrs_steady --n 15 --N 500000 --censor 0.3 --method MHRS --warmup 200 --steps 100
 run cfg5_dcs --n 15 --N 500000 --censor 0.3 --method DCS --steps 50
-run cfg5_ecs --n 15 --N 500000 --censor 0.3 --method ECS --steps 10
+run cfg5_ecs --n 15 --N 500000 --censor 0.3 --method ECS --steps 20
 run cfg3_unif --n 20 --N 100000 --method UNIF --steps 50
 run cfg5_unif --n 15 --N 500000 --censor 0.3 --method UNIF --steps 20
 python3 - $O <<'PY'
