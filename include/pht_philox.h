@@ -95,7 +95,14 @@ PHT_HD2 void pht_stream_init_block0(pht_stream *s, uint32_t k0, uint32_t k1, uin
 
 PHT_HD2 pht_u32x4 pht_stream_block(pht_stream *s) {
   pht_u32x4 c; c.v[0] = s->obs; c.v[1] = s->tag; c.v[2] = s->sweep; c.v[3] = s->blk++;
+#if defined(__HIP_DEVICE_COMPILE__)
+  /* every stream a wavefront holds carries its launch's key (SweepArgs k0/k1,
+   * one per workgroup): read it as a wave-uniform value, so that the key
+   * schedule runs on the scalar unit and the rounds' xors take it from SGPRs */
+  return pht_philox4x32_10(c, __builtin_amdgcn_readfirstlane(s->k0), __builtin_amdgcn_readfirstlane(s->k1));
+#else
   return pht_philox4x32_10(c, s->k0, s->k1);
+#endif
 }
 
 /* generate the next block ahead (no effect on the word sequence) */
