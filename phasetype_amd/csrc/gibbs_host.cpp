@@ -153,11 +153,19 @@ typedef void (*dgetri_t)(const int *, double *, const int *, const int *, double
 dgeevx_t p_dgeevx = nullptr;
 dgetrf_t p_dgetrf = nullptr;
 dgetri_t p_dgetri = nullptr;
+/* OpenBLAS's thread-count setter, when the bound LAPACK is OpenBLAS (returns
+ * the previous count).  The per-sweep eigensystem is an n <= 20 problem: its
+ * BLAS calls gain nothing from the thread pool and pay its hand-offs (n = 10:
+ * 81 us per parameter block with the pool, 17 us on the calling thread; the
+ * same bytes, tests/test_host.py) */
+typedef int (*blas_threads_t)(int);
+blas_threads_t p_blas_threads = nullptr;
 
 bool lookup_lapack(void *h) {
   p_dgeevx = (dgeevx_t)dlsym(h, "dgeevx_");
   p_dgetrf = (dgetrf_t)dlsym(h, "dgetrf_");
   p_dgetri = (dgetri_t)dlsym(h, "dgetri_");
+  p_blas_threads = (blas_threads_t)dlsym(h, "openblas_set_num_threads_local");
   if (p_dgeevx && p_dgetrf && p_dgetri) return true;
   p_dgeevx = nullptr;
   return false;
@@ -196,6 +204,7 @@ extern "C" int pht_bind_lapack(const char *path, const char *prefix) {
   p_dgeevx = (dgeevx_t)dlsym(h, (pre + "dgeevx_").c_str());
   p_dgetrf = (dgetrf_t)dlsym(h, (pre + "dgetrf_").c_str());
   p_dgetri = (dgetri_t)dlsym(h, (pre + "dgetri_").c_str());
+  p_blas_threads = (blas_threads_t)dlsym(h, "openblas_set_num_threads_local");
   if (!(p_dgeevx && p_dgetrf && p_dgetri)) {
     p_dgeevx = nullptr;
     set_err("LAPACK symbols %sdgeevx_/dgetrf_/dgetri_ not found in %s", pre.c_str(), path);
@@ -206,7 +215,22 @@ extern "C" int pht_bind_lapack(const char *path, const char *prefix) {
 
 /* LJMA_eigen with LJMA_Gibbs's workspace sizing (src/utility.c:87-129,
  * src/PHT_MCMC_Aslett.c:177-185). */
+/* the bound OpenBLAS on one thread for the duration of a scope (the
+ * outermost one sets and restores: a Gibbs run once, a lone eigen() call
+ * per call) */
+static thread_local int g_blas_one = 0;
+struct OneBlasThread {
+  int prev = 0;
+  OneBlasThread() {
+    if (g_blas_one++ == 0 && p_blas_threads) prev = p_blas_threads(1);
+  }
+  ~OneBlasThread() {
+    if (--g_blas_one == 0 && p_blas_threads && prev > 1) p_blas_threads(prev);
+  }
+};
+
 static int eigen(int n, const double *S, double *evals, double *Q, double *Qinv) {
+  OneBlasThread one;
   char balanc = 'B', jobv = 'V', sense = 'B';
   int lwork = -1, info = 0, ilo, ihi, nn = n;
   double wq = 0, abnrm;
@@ -1400,6 +1424,7 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
               void *reduce_user, double *kernel_ms_total) {
   (void)y; (void)l; (void)mhit;
   GibbsState G(R, it, n, m, nu, zeta, T, C, start, res);
+  OneBlasThread one; /* the per-sweep eigensystems on this thread */
   const int disp = dispatch_method(method);
   const int sl = stats_len(n);
   std::vector<long long> tot(sl);
