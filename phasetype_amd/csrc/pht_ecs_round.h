@@ -28,6 +28,16 @@
 namespace pht {
 
 constexpr int kRoundCap = 13; /* envelope points handled by the converged code */
+template <class Env>
+constexpr bool round_env_ok() { return Env::kLds == 0 || Env::kLds >= kRoundCap; }
+/* run-time envelope positions of the converged round (invert's segment, the
+ * insert's neighbours and new point) read through the LDS-only accessors
+ * (no private-memory branch: ~900 instructions less per kernel; cfg5 ECS
+ * -2.0 %, the 125k shard -1.6 %, cfg4 -0.1 %); not at n = 20, where the
+ * allocator then spills 74 VGPRs instead of 43 in the one-lane body (cfg3
+ * +1.2 %; profiles/r05/env_lds_only/) */
+template <int NT>
+constexpr bool round_lds_only() { return NT > 0 && NT < 20; }
 
 /*
  * All intersection points (even positions) of an envelope of at most CAP
@@ -150,7 +160,7 @@ __device__ __forceinline__ void round_cumulate(Env &e, double *cs) {
 
 /* arms_invert with the unrolled scan over cs[] (registers); the segment's
  * ends are tracked along the scan; ey of the two ends recomputed */
-template <int CAP, class Env>
+template <int CAP, bool LD, class Env>
 __device__ __forceinline__ void round_invert(Env &e, const double *cs, double prob, WPt &p) {
   const int last = e.cnt - 1;
   /* cum at last and last - 1 (the segment's ends before the scan moves) */
@@ -176,8 +186,9 @@ __device__ __forceinline__ void round_invert(Env &e, const double *cs, double pr
   }
   p.pr = q;
   const double prop = PHT_DIV((u - cl), (cr - cl));
-  const double xl = e.X(q - 1), xr = e.X(q);
-  const double yr = e.Y(q), yl = e.Y(q - 1);
+  /* (1 <= q <= last < CAP <= the LDS points) */
+  const double xl = LD ? e.XL(q - 1) : e.X(q - 1), xr = LD ? e.XL(q) : e.X(q);
+  const double yr = LD ? e.YL(q) : e.Y(q), yl = LD ? e.YL(q - 1) : e.Y(q - 1);
   const double eyr = expshift_le(yr, e.ymax);
   /* the point is built in scalars and stored once: assigning p's fields in
    * both branches let the compiler merge them into one store through a
@@ -209,7 +220,7 @@ __device__ __forceinline__ void round_invert(Env &e, const double *cs, double pr
 /* the first half of arms_update (shift + insert + XEPS adjustment), for an
  * envelope that stays within kRoundCap points; meets and cumulate follow
  * in the converged block */
-template <int CAP, class Env, class F>
+template <int CAP, bool LD, class Env, class F>
 __device__ __forceinline__ void round_insert(Env &e, const ArmsPend &pd, F &f, Lane &ln) {
   /* cnt + 2 <= CAP */
   const int pr = pd.pr;
@@ -221,7 +232,8 @@ __device__ __forceinline__ void round_insert(Env &e, const ArmsPend &pd, F &f, L
    * (new position m holds old m - 2 where the shift moves it, else old m;
    * ql < qi < qr, so neither is the new point): no store -> load wait */
   auto src = [&](int m) { return (m >= 2 && m - 2 >= pr && m - 2 <= last) ? m - 2 : m; };
-  const double xl = e.X(src(ql)), xr = e.X(src(qr));
+  /* (every position here is < CAP <= the LDS points) */
+  const double xl = LD ? e.XL(src(ql)) : e.X(src(ql)), xr = LD ? e.XL(src(qr)) : e.X(src(qr));
   double xs[CAP], ys[CAP];
 #pragma unroll
   for (int k = 0; k + 2 < CAP; k++) {
@@ -238,17 +250,23 @@ __device__ __forceinline__ void round_insert(Env &e, const ArmsPend &pd, F &f, L
     }
   }
   e.cnt += 2;
-  e.sX(qi, pd.px);
-  e.sY(qi, pd.py);
+  auto put = [&](double x, double y) {
+    if constexpr (LD) {
+      e.sXL(qi, x);
+      e.sYL(qi, y);
+    } else {
+      e.sX(qi, x);
+      e.sY(qi, y);
+    }
+  };
+  put(pd.px, pd.py);
   if (pd.px < (1. - kXEps) * xl + kXEps * xr) {
     const double xn = (1. - kXEps) * xl + kXEps * xr;
-    e.sX(qi, xn);
-    e.sY(qi, f(xn));
+    put(xn, f(xn));
     ln.neval++;
   } else if (pd.px > kXEps * xl + (1. - kXEps) * xr) {
     const double xn = kXEps * xl + (1. - kXEps) * xr;
-    e.sX(qi, xn);
-    e.sY(qi, f(xn));
+    put(xn, f(xn));
     ln.neval++;
   }
 }
@@ -287,6 +305,7 @@ __device__ __forceinline__ double round_metropolis(const Env &e, const WPt &p, d
 template <int NT, class Env, class Sink>
 __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st, bool start,
                                           bool &pend, ArmsPend &pd, double lam, bool &obsdone) {
+  static_assert(round_env_ok<Env>(), "the converged round's positions must lie in the LDS part");
   const int n = P.n();
   const double y_t = st.yt;
   const int j = st.j;
@@ -357,9 +376,9 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
   /* ---- pending lanes: the update that ends the rejected iteration */
   if (pend) big = (env.cnt + 2 > kRoundCap);
   if (__any(pend && !big && env.cnt > 9)) {
-    if (pend && !big) round_insert<13>(env, pd, f, ln);
+    if (pend && !big) round_insert<13, round_lds_only<NT>()>(env, pd, f, ln);
   } else {
-    if (pend && !big) round_insert<11>(env, pd, f, ln);
+    if (pend && !big) round_insert<11, round_lds_only<NT>()>(env, pd, f, ln);
   }
   PHT_STAMP(ln, 3);
   /* ---- converged: intersections and areas over the widest envelope in
@@ -397,9 +416,10 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
   double yv = 0.0, ynew = 0.0;
   if (itr) {
     const double pu = dev_u(ln.r);
-    if (cap == 9) round_invert<9>(env, cs, pu, q);
-    else if (cap == 11) round_invert<11>(env, cs, pu, q);
-    else round_invert<13>(env, cs, pu, q);
+    constexpr bool LD = round_lds_only<NT>();
+    if (cap == 9) round_invert<9, LD>(env, cs, pu, q);
+    else if (cap == 11) round_invert<11, LD>(env, cs, pu, q);
+    else round_invert<13, LD>(env, cs, pu, q);
     const double u = dev_u(ln.r) * q.ey;
     yv = logshift(u, env.ymax);
   }

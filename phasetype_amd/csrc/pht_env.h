@@ -37,6 +37,11 @@ struct EnvPrivate {
   __device__ __forceinline__ void sX(int k, double v) { x[k] = v; }
   __device__ __forceinline__ void sY(int k, double v) { y[k] = v; }
   __device__ __forceinline__ void sCUM(int k, double v) { cum[k] = v; }
+  /* positions known to lie below kLds (EnvLdsXY): the same storage here */
+  __device__ __forceinline__ double XL(int k) const { return x[k]; }
+  __device__ __forceinline__ double YL(int k) const { return y[k]; }
+  __device__ __forceinline__ void sXL(int k, double v) { x[k] = v; }
+  __device__ __forceinline__ void sYL(int k, double v) { y[k] = v; }
 };
 
 /* EnvPrivate for envelopes known to exceed kArmsU points (the ECS row
@@ -79,6 +84,12 @@ struct EnvLdsXY {
     if (k < K) l[(K + k) * STRIDE] = v; else ov[kSpill + k - K] = v;
   }
   __device__ __forceinline__ void sCUM(int k, double v) { cm[k] = v; }
+  /* run-time positions the caller knows to be < K (the converged round's
+   * envelope, pht_ecs_round.h): LDS only, no private-memory branch */
+  __device__ __forceinline__ double XL(int k) const { return l[k * STRIDE]; }
+  __device__ __forceinline__ double YL(int k) const { return l[(K + k) * STRIDE]; }
+  __device__ __forceinline__ void sXL(int k, double v) { l[k * STRIDE] = v; }
+  __device__ __forceinline__ void sYL(int k, double v) { l[(K + k) * STRIDE] = v; }
 };
 
 }  // namespace pht
