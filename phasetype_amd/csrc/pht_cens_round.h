@@ -3,16 +3,16 @@
  * (LJMA_samplechain + LJMA_condjump_r_ars, src/Simulate_AbsCTMC_gt_Aslett_DCS.c:
  * 184-260, 299-418) as a persistent kernel of jump-converged rounds.
  *
- * One lane running censored() to the end of its path idles, once its path
+ * One lane running a censored path to its end idles, once its path
  * is done, until the longest path of its wavefront is (a censored path
  * runs past y until absorption, so path lengths vary widely).  Here a loop
  * iteration ("round") is ONE jump of every lane (censored_jump in
  * pht_device.h: the sojourn by the stay test / ARMS / exponential, then
  * the next state); a lane whose path ended takes the next observation at
  * the top of the next round and makes its first jump in that round.
- * Every lane performs exactly censored()'s operations and draws: results
- * are bit-identical to the one-lane kernel and to the oracle's device
- * specification (orcD_censored).  The launch must hold censored
+ * Every lane performs exactly the device specification's operations and
+ * draws (censored_begin + censored_jump until done): results are
+ * bit-identical to the oracle's device specification (orcD_censored).  The launch must hold censored
  * observations only (SweepArgs::allcens; ctx_enqueue's censored range).
  */
 #ifndef PHT_CENS_ROUND_H

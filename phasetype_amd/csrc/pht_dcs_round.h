@@ -2,14 +2,14 @@
  * pht_dcs_round.h — the DCS sampler (method 4) as a persistent kernel of
  * jump-converged rounds.
  *
- * The path of an observation (dcs() in pht_device.h: LJMA_Hobolth_endState +
+ * The path of an observation (LJMA_Hobolth_endState +
  * LJMA_samplechain_Hobolth + HobCDF + Find02,
  * src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:11-51,
  * src/Simulate_AbsCTMC_gt_Hobolth_DCS.c:23-226, src/utility.c:233-338) is a
  * sequence of jumps (5.4 on average at cfg5-shaped n = 10, up to ~30), each
  * a set-up (E = e^{lambda x}, the exit test, the next state) and a Brent
  * search on HobCDF (~11 CDF evaluations).  With one lane per observation
- * running dcs() to its end, a lane whose path is short idles until the
+ * running its whole path, a lane whose path is short idles until the
  * longest path of its wavefront is done.  Here a loop iteration ("round")
  * is ONE jump of every lane; a lane whose path ended takes the next
  * observation at the top of the next round (its end state and start state,
@@ -18,10 +18,11 @@
  * e^{lambda_i (y - t)} serve both a new observation's end state (t = 0) and
  * the jump's E.
  *
- * Every lane performs exactly dcs()'s operations on exactly its values, in
- * the same order, and draws the same words: results are bit-identical to
- * the one-lane kernel and to the oracle's device specification
- * (oracle/pht_oracle_impl.h, orcD_dcs).  Per-sweep n x n tables, computed
+ * Every lane performs exactly the device specification's operations on
+ * exactly its values, in the same order, and draws the same words: results
+ * are bit-identical to the oracle's device specification
+ * (oracle/pht_oracle_impl.h, orcD_dcs; the round-1 one-lane kernel that ran
+ * the same path to its end was retired in r05).  Per-sweep n x n tables, computed
  * once per workgroup into LDS, take the divisions out of the CDF
  * evaluations: the near-equal-eigenvalue test |(lambda_i - S_jj) / S_jj| <
  * 1e-13 (same values), and 1 / (lambda_i - S_jj), which the device spec
@@ -52,14 +53,14 @@ enum : int { kDcsFree = 0, kDcsSetup = 1, kDcsNew = 3, kDcsDone = 4 };
  * run it as a state machine, because PHT_DCS_ROOT=brent must reproduce the
  * reference's root bit for bit (the default root is hob_halley).
  *
- * Find02's state between CDF evaluations (find02 in pht_device.h); tol = 0
- * as dcs() calls it */
+ * Find02's state between CDF evaluations; tol = 0 and maxit = 1000 as the
+ * reference calls it (src/Simulate_AbsCTMC_gt_Hobolth_DCS.c) */
 struct BrentSt {
   double a, b, c, fa, fb, fc;
   int maxit;
 };
 
-/* find02's loop head, up to the next evaluation point: returns true when
+/* Find02's loop head, up to the next evaluation point: returns true when
  * the search is over (root in `root`), false with b advanced (evaluate f(b)) */
 __device__ __forceinline__ bool brent_head(BrentSt &s, double &root) {
   const double tol = 0.0;
@@ -100,7 +101,7 @@ __device__ __forceinline__ bool brent_head(BrentSt &s, double &root) {
   return false;
 }
 
-/* find02's loop tail after fb = f(b) */
+/* Find02's loop tail after fb = f(b) */
 __device__ __forceinline__ void brent_tail(BrentSt &s, double fb) {
   s.fb = fb;
   if ((s.fb > 0 && s.fc > 0) || (s.fb < 0 && s.fc < 0)) {
@@ -254,7 +255,8 @@ __device__ __forceinline__ double hob_halley(const Par<NT> &P, const DcsE<NT> &E
  * src/Simulate_AbsCTMC_eq_AslettHobolth_DCS.c:11-51) from ey_i = e^{lambda_i
  * y} and the target uniform u: shared by the round kernel and the end-state
  * pre-pass (dcs_end_kernel), so both give the same b bit for bit.  (The
- * weights are recomputed in the scan, as dcs() does.) */
+ * weights are recomputed in the scan instead of kept in registers: the
+ * same operations, so the same values.) */
 template <int NT, class EV>
 __device__ __forceinline__ int dcs_end_state(const Par<NT> &P, const EV &ey, double u, int &flags) {
   const int n = P.n();
@@ -396,7 +398,8 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
     c_brent += (unsigned)ln.nbrent;
     st.phase = kDcsFree;
   };
-  /* the head of dcs()'s jump loop (while (t < y) { if (njump++ >= cap) ...) */
+  /* the head of the path's jump loop (while (t < y) { if (njump++ >= cap) ...),
+   * src/Simulate_AbsCTMC_gt_Hobolth_DCS.c */
   auto jump_head = [&]() {
     if (!(st.t < st.y)) { /* the loop condition (t < y always holds after a jump) */
       finish_obs();
@@ -431,7 +434,7 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
     st.njump = 0;
     jump_head(); /* t = 0 < y unless y <= 0 */
   };
-  /* the end of a jump: find02's root through dcs()'s halving guard, the
+  /* the end of a jump: Find02's root through the reference's halving guard, the
    * statistics, the next loop head */
   auto end_jump = [&](double root) {
     double jtime = root;
@@ -491,7 +494,7 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
      * the jump loop's head */
     if (st.phase == kDcsNew) new_obs(e);
 
-    /* ---- one jump of every active lane (dcs()'s loop body) */
+    /* ---- one jump of every active lane (the jump loop's body) */
     if (st.phase == kDcsSetup) {
       const int j = st.j;
       const double x = st.y - st.t;
@@ -562,7 +565,7 @@ __device__ __forceinline__ void dcs_round_body(const SweepArgs &a, unsigned blk,
           if (!a.dcsbrent) {
             root = hob_halley<NT>(P, E, rinv + j * n, near, Sjj, x, es, coef, u, jn, st.b, wl, ln);
           } else {
-          /* find02(0, y - t, -u, 1 - u, HobCDF, Tol = 0, Maxit = 1000) */
+          /* Find02(0, y - t, -u, 1 - u, HobCDF, Tol = 0, Maxit = 1000) */
           BrentSt bs;
           bs.a = 0.0;
           bs.b = st.y - st.t;

@@ -820,35 +820,6 @@ __device__ __forceinline__ EcsDens<NT> ecs_dens(const Par<NT> &P, EcsLane<NT> &s
   return ecs_dens(P, st, lam_max(P));
 }
 
-/* one complete non-absorbing jump: ARMS sojourn (:307-342), moveMass and
- * the categorical (ecs_jump_finish).  The persistent kernel runs the same
- * steps in converged rounds (pht_ecs_round.h). */
-template <int NT, class Env, class Sink>
-__device__ __forceinline__ void ecs_jump(const Par<NT> &P, Lane &ln, Env &env, Sink &sk, EcsLane<NT> &st) {
-  const int n = P.n();
-  const double y_t = st.yt;
-  if (!st.haveE0) { /* s_j = 0 at the first sojourn: no absorb test ran */
-    ecs_first_E0(P, y_t, lam_max(P), st.E0);
-    st.haveE0 = true;
-  }
-  EcsDens<NT> f = ecs_dens(P, st);
-  double xinit[4];
-  xinit[0] = (y_t) / 1e6;
-  xinit[1] = (y_t) / 3.0;
-  xinit[2] = xinit[1] * 2.0;
-  xinit[3] = y_t - xinit[0];
-  double xsamp = 0.0;
-  const int ainfo = arms(env, xinit, 0.0, y_t, f, 0.0, xsamp, ln);
-  ecs_jump_finish(P, ln, sk, st, f, xsamp, ainfo);
-}
-
-template <int NT, class Env, class Sink>
-__device__ __forceinline__ void ecs_exact(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
-  EcsLane<NT> st;
-  ecs_begin(P, y, ln, sk, st);
-  while (!ecs_try_absorb(P, ln, sk, st)) ecs_jump(P, ln, env, sk, st);
-}
-
 /* ===================================================== censored path */
 /*
  * Device specification of the censored path (r05, "v2"; the oracle's dev
@@ -1077,14 +1048,6 @@ __device__ __forceinline__ bool censored_jump(const Par<NT> &P, Lane &ln, Env &e
   return done;
 }
 
-template <int NT, class Env, class Sink>
-__device__ __forceinline__ void censored(const Par<NT> &P, double y, Lane &ln, Env &env, Sink &sk) {
-  CensLane<NT> c;
-  censored_begin(P, y, ln, sk, c);
-  while (!censored_jump(P, ln, env, sk, c)) {
-  }
-}
-
 /* ================================================================ MHRS */
 /*
  * Device specification of LJMA_MHsample_Bladt / LJMA_samplechain_Bladt
@@ -1175,202 +1138,6 @@ __device__ __forceinline__ bool mhrs_try(const Par<NT> &P, double y, int cens, u
   int fl = 0, nj = 0;
   NoSink ns;
   return mhrs_attempt<NT, false>(P, y, cens, r, pre, fl, nj, ns);
-}
-
-/* ================================================================= DCS */
-template <int NT>
-struct HobCdf {
-  const Par<NT> &P;
-  int lastj, j;
-  double prob, Pab, y, t, u, Sll, coef;
-  const double *E, *Qb;
-  __device__ __forceinline__ double operator()(double x) const {
-    const int n = P.n();
-    double tmp = 0.0;
-#pragma unroll
-    for (int i = 0; i < n; i++) {
-      const double ev = P.evals(i), Ei = E[i];
-      double Ji;
-      if (fabs((ev - Sll) / Sll) < 1e-13) Ji = x * Ei;
-      else Ji = (Ei - pht_exp_neg((y - t - x) * ev + Sll * x)) * (1.0 / (ev - Sll));
-      tmp = fma(P.Q(j, i) * Ji, Qb[i], tmp);
-    }
-    return 1 / prob * P.S(lastj, j) / Pab * tmp - u;
-  }
-};
-
-/* Provenance: Brent's zeroin as in R core's src/library/stats/src/zeroin.c
- * (R_zeroin2; GPL-2), which the reference carries as Find02
- * (src/utility.c:233-338).  Its statement order is kept because the device
- * spec must reproduce the reference's root bit for bit.  Used only by the
- * round-1 one-lane DCS kernel (PHT_LEGACY_KERNELS builds); the round kernel
- * splits the same iteration into brent_head/brent_tail (pht_dcs_round.h). */
-template <class F>
-__device__ __forceinline__ double find02(double ax, double bx, double fa, double fb, const F &f, double *Tol, int *Maxit,
-                         int &nevals) {
-  double a, b, c, fc, tol;
-  int maxit;
-  a = ax; b = bx;
-  c = a; fc = fa;
-  maxit = *Maxit + 1; tol = *Tol;
-  if (fa == 0.0) { *Tol = 0.0; *Maxit = 0; return a; }
-  if (fb == 0.0) { *Tol = 0.0; *Maxit = 0; return b; }
-  while (maxit--) {
-    double prev_step = b - a, tol_act, p, q, new_step;
-    if (fabs(fc) < fabs(fb)) {
-      a = b; b = c; c = a;
-      fa = fb; fb = fc; fc = fa;
-    }
-    tol_act = 2 * 2.2204460492503131e-16 * fabs(b) + tol / 2;
-    new_step = (c - b) / 2;
-    if (fabs(new_step) <= tol_act || fb == (double)0) {
-      *Maxit -= maxit;
-      *Tol = fabs(c - b);
-      return b;
-    }
-    if (fabs(prev_step) >= tol_act && fabs(fa) > fabs(fb)) {
-      double t1, cb, t2;
-      cb = c - b;
-      if (a == c) {
-        t1 = fb / fa;
-        p = cb * t1;
-        q = 1.0 - t1;
-      } else {
-        q = fa / fc; t1 = fb / fc; t2 = fb / fa;
-        p = t2 * (cb * q * (q - t1) - (b - a) * (t1 - 1.0));
-        q = (q - 1.0) * (t1 - 1.0) * (t2 - 1.0);
-      }
-      if (p > (double)0) q = -q;
-      else p = -p;
-      if (p < (0.75 * cb * q - fabs(tol_act * q) / 2) && p < fabs(prev_step * q / 2)) new_step = p / q;
-    }
-    if (fabs(new_step) < tol_act) new_step = (new_step > (double)0) ? tol_act : -tol_act;
-    a = b; fa = fb;
-    b += new_step; fb = f(b);
-    nevals++;
-    if ((fb > 0 && fc > 0) || (fb < 0 && fc < 0)) { c = a; fc = fa; }
-  }
-  *Tol = fabs(c - b);
-  *Maxit = -1;
-  return b;
-}
-
-template <int NT, class Sink>
-__device__ __forceinline__ void dcs(const Par<NT> &P, double y, Lane &ln, Sink &sk) {
-  const int n = P.n();
-  /* end state b ~ (pi e^{yS})_b s_b */
-  double a[PHT_VEC(NT)];
-#pragma unroll
-  for (int i = 0; i < n; i++) a[i] = P.piQ(i) * pht_exp_neg(P.evals(i) * y);
-  int b;
-  {
-    /* end-state weights pend_k = (a Qinv)_k s_k, recomputed in the scan
-     * instead of kept in registers (same operations, so the same values):
-     * the kernel's register peak is here, outside the jump loop */
-    double sum = 0.0;
-#pragma unroll 1
-    for (int k = 0; k < n; k++) {
-      double acc = 0.0;
-#pragma unroll
-      for (int i = 0; i < n; i++) acc = fma(a[i], P.Qinv(i, k), acc);
-      sum += acc * P.s(k);
-    }
-    const double tg = dev_u(ln.r) * sum;
-    double sofar = 0.0;
-    int q = 0;
-#pragma unroll 1
-    for (; q < n; q++) {
-      double acc = 0.0;
-#pragma unroll
-      for (int i = 0; i < n; i++) acc = fma(a[i], P.Qinv(i, q), acc);
-      sofar += acc * P.s(q);
-      if (!(sofar < tg)) break;
-    }
-    if (q == n) {
-      ln.flags |= kFlagScanEnd;
-      q = n - 1;
-    }
-    b = q;
-  }
-  double Qb[PHT_VEC(NT)];
-#pragma unroll
-  for (int i = 0; i < n; i++) Qb[i] = P.Qinv(i, b);
-  double target = dev_u(ln.r);
-  const int B = pistart(P, target, ln.flags);
-  sk.start(B);
-  double t = 0.0, jtime = 0.0;
-  int j = B, lastj, njump = 0;
-  while (t < y) {
-    if (njump++ >= kMaxJumps) {
-      ln.flags |= kFlagJumpCap;
-      break;
-    }
-    lastj = j;
-    const double x = y - t;
-    const double Sjj = P.S(j, j);
-    double E[PHT_VEC(NT)];
-#pragma unroll
-    for (int i = 0; i < n; i++) E[i] = pht_exp_neg(P.evals(i) * x);
-    double Pab = 0.0;
-#pragma unroll
-    for (int i = 0; i < n; i++) Pab = fma(P.Q(j, i) * E[i], Qb[i], Pab);
-    if (j == b) {
-      if (dev_runif(ln.r, 0.0, 1.0) < pht_exp_neg(Sjj * (y - t)) / Pab) {
-        sk.z(j, (y - t));
-        sk.N(j, j);
-        sk.pre(j);
-        return;
-      }
-    }
-    double J[PHT_VEC(NT)];
-#pragma unroll
-    for (int i = 0; i < n; i++) {
-      const double ev = P.evals(i);
-      if (fabs((ev - Sjj) / Sjj) < 1e-13) J[i] = x * E[i];
-      else J[i] = (E[i] - pht_exp_neg(Sjj * x)) * (1.0 / (ev - Sjj));
-    }
-    const int cnt = P.nsuccS(j);
-    double pw[PHT_VEC(NT)];
-    double p_sum = 0.0;
-    for (int q = 0; q < cnt; q++) {
-      const int i = P.succS(j, q);
-      double tmp = 0.0;
-#pragma unroll
-      for (int k = 0; k < n; k++) tmp = fma(P.Q(i, k) * J[k], Qb[k], tmp);
-      p_sum += pw[q] = P.S(j, i) / Pab * tmp;
-    }
-    target = dev_runif(ln.r, 0.0, p_sum);
-    if (!(target > 0.0)) {
-      ln.flags |= kFlagDcsZero;
-      sk.pre(j);
-      return;
-    }
-    double prob;
-    {
-      double sofar = 0.0;
-      int q = 0;
-      for (; q < cnt; q++) {
-        sofar += pw[q];
-        if (!(sofar < target)) break;
-      }
-      if (q == cnt) {
-        ln.flags |= kFlagScanEnd;
-        q = cnt - 1;
-      }
-      j = P.succS(j, q);
-      prob = pw[q];
-    }
-    HobCdf<NT> hc{P, lastj, j, prob, Pab, y, t, 0.0, Sjj, 0.0, E, Qb};
-    hc.u = dev_runif(ln.r, 0.0, 1.0);
-    double Tol = 0.0;
-    int Maxit = 1000;
-    jtime = find02(0.0, y - t, -hc.u, 1.0 - hc.u, hc, &Tol, &Maxit, ln.nbrent);
-    while (t + jtime >= y) jtime = jtime / 2;
-    sk.N(lastj, j);
-    sk.z(lastj, jtime);
-    t += jtime;
-    ln.njump++;
-  }
 }
 
 }  // namespace pht

@@ -476,12 +476,11 @@ __device__ __forceinline__ void mhrs_finish(const Par<NT> &P, const SweepArgs &a
   ln.neval = (int)natt;
 }
 
-/* One lane per observation (PERSIST false: lane = launch position), or
- * persistent lanes (PERSIST true: a lane claims the next 64-position chunk
- * slot through an LDS cursor as soon as its observation is done, so a
- * wavefront never waits on its longest path; DCS and the censored range). */
-template <int NT, int METHOD, bool DEBUG, class Env, bool PERSIST = false>
-__device__ __forceinline__ void sweep_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
+/* MHRS's MH decisions and the accepted attempt's replay, one observation per
+ * lane on a persistent grid: a lane claims the next 64-position chunk slot
+ * through an LDS cursor as soon as its observation is done. */
+template <int NT, bool DEBUG>
+__device__ __forceinline__ void mhrs_finish_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
   const Layout L = make_layout(n);
@@ -501,7 +500,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, unsigned blk, uns
   pht_stage_math_tables();
   for (int k = threadIdx.x; k < n + kStatExtra; k += blockDim.x) zq[k] = 0ull;
   for (int k = threadIdx.x; k < n + n * n; k += blockDim.x) Bc[k] = 0u;
-  if (PERSIST && threadIdx.x == 0) *cursor = 0;
+  if (threadIdx.x == 0) *cursor = 0;
   __syncthreads();
 
   Par<NT> P;
@@ -509,16 +508,11 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, unsigned blk, uns
   P.iv = (const PHT_LDS int *)(lsm + L.ndouble * 8);
   P.Lr = L;
 
-  long i = a.begin + (long)blk * blockDim.x + threadIdx.x;
   for (;;) {
-    if (PERSIST) {
-      const long t = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const long p = claim_pos(t, blk, nblk);
-      if (p >= a.count) break;
-      i = a.begin + p;
-    } else if (i >= a.begin + a.count) {
-      break;
-    }
+    const long t = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const long p = claim_pos(t, blk, nblk);
+    if (p >= a.count) break;
+    const long i = a.begin + p;
     Lane ln;
     pht_stream_init(&ln.r, a.k0, a.k1, a.gid[i], 0u, a.sweep);
     ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
@@ -529,18 +523,9 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, unsigned blk, uns
       sk.dB = a.dbg_B + i;
       sk.dpre = a.dbg_pre + i;
     }
-    const double y = a.y[i];
-    Env env;
-    if (METHOD == kMethodMHRS) {
-      mhrs_finish<NT>(P, a, i, y, a.cens[i], ln, sk);
-    } else if (METHOD == kMethodDCS) {
-      dcs<NT>(P, y, ln, sk);
-    } else {
-      if (a.cens[i]) censored<NT>(P, y, ln, env, sk);
-      else ecs_exact<NT>(P, y, ln, env, sk);
-    }
-    /* draws: stream words; MHRS: + attempts (ln.neval, see mhrs_finish) */
-    const uint32_t nd = pht_stream_pos(&ln.r) + (METHOD == kMethodMHRS ? (uint32_t)ln.neval : 0u);
+    mhrs_finish<NT>(P, a, i, a.y[i], a.cens[i], ln, sk);
+    /* draws: stream words + attempts (ln.neval, see mhrs_finish) */
+    const uint32_t nd = pht_stream_pos(&ln.r) + (uint32_t)ln.neval;
     if (DEBUG) {
       a.dbg_flags[i] = ln.flags;
       a.dbg_ndraw[i] = nd;
@@ -551,16 +536,10 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, unsigned blk, uns
     lds_add(&xc[3], (unsigned long long)nd);
     lds_add(&xc[4], (unsigned long long)ln.njump);
     lds_add(&xc[5], (unsigned long long)ln.nbrent);
-    if (!PERSIST) break;
   }
   __syncthreads();
   /* flush: [zq n][B n][N n*n][extra] */
   flush_stats(a.stats, zq, Bc, Nc, xc, n);
-}
-
-template <int NT, int METHOD, bool DEBUG>
-__global__ void __launch_bounds__(kBlock) sweep_kernel(SweepArgs a) {
-  sweep_body<NT, METHOD, DEBUG, EnvPrivate>(a, blockIdx.x, gridDim.x);
 }
 
 /* MHRS's finish (MH decisions + the accepted attempt replayed) on a
@@ -569,7 +548,7 @@ __global__ void __launch_bounds__(kBlock) sweep_kernel(SweepArgs a) {
  * words into the same global block (~500k same-address atomics per sweep) */
 template <int NT, bool DEBUG>
 __global__ void __launch_bounds__(kBlock) mhrs_finish_kernel(SweepArgs a) {
-  sweep_body<NT, kMethodMHRS, DEBUG, EnvPrivate, true>(a, blockIdx.x, gridDim.x);
+  mhrs_finish_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
 }
 
 /* waves per SIMD the persistent kernel is compiled for: the DCS kernel at
@@ -584,18 +563,6 @@ template <int NT, int METHOD>
 constexpr int persist_waves() {
   return PHT_PERSIST_WAVES > 0 ? PHT_PERSIST_WAVES : ((NT == 10 && METHOD == kMethodDCS) ? 2 : 1);
 }
-#ifdef PHT_LEGACY_KERNELS
-/* the one-lane-to-the-end DCS and censored-ECS kernels of round 1, kept only
- * for A/B against the round kernels (tools/build_variant.py -D
- * PHT_LEGACY_KERNELS; PHT_DCS_KERNEL / PHT_CENS_KERNEL=legacy) */
-template <int NT, int METHOD, bool DEBUG>
-__global__ void __launch_bounds__(kBlock)
-__attribute__((amdgpu_waves_per_eu(persist_waves<NT, METHOD>())))
-persist_kernel(SweepArgs a) {
-  sweep_body<NT, METHOD, DEBUG, EnvPrivate, true>(a, blockIdx.x, gridDim.x);
-}
-#endif
-
 /* LDS bytes a workgroup needs: parameter block + accumulators (+ cursor) */
 static int smem_bytes(int n) {
   const Layout L = make_layout(n);
@@ -644,25 +611,6 @@ static hipError_t launch_config(LaunchCfg &cfg, const void *kernel, int sm, int 
   *cus = c.cus;
   return hipSuccess;
 }
-
-#ifdef PHT_LEGACY_KERNELS
-/* persistent one-lane kernels: grid = CUs x occupancy, capped by the work */
-template <int NT, int METHOD, bool DEBUG>
-static hipError_t launch_persist(const SweepArgs &a, hipStream_t st) {
-  static LaunchCfg cfg;
-  const int sm = smem_bytes(a.n);
-  int occ = 0, cus = 0;
-  if (hipError_t e = launch_config(cfg, (const void *)persist_kernel<NT, METHOD, DEBUG>, sm, &occ, &cus);
-      e != hipSuccess)
-    return e;
-  long grid = (long)cus * occ;
-  const long want = (a.count + kBlock - 1) / kBlock;
-  if (grid > want) grid = want;
-  if (grid < 1) return hipSuccess;
-  hipLaunchKernelGGL((persist_kernel<NT, METHOD, DEBUG>), dim3((unsigned)grid), dim3(kBlock), sm, st, a);
-  return hipGetLastError();
-}
-#endif
 
 /*
  * ECS exact observations, persistent lanes.  Block b owns chunks of 64
@@ -1748,21 +1696,6 @@ static hipError_t launch_unif(const SweepArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
-/* PHT_CENS_KERNEL=legacy / PHT_DCS_KERNEL=legacy: the round-1 one-lane
- * kernels (A/B only; a library built without PHT_LEGACY_KERNELS refuses) */
-static bool env_legacy(const char *name) {
-  const char *e = getenv(name);
-  return e && !strcmp(e, "legacy");
-}
-static bool cens_legacy() {
-  static const bool v = env_legacy("PHT_CENS_KERNEL");
-  return v;
-}
-static bool dcs_legacy() {
-  static const bool v = env_legacy("PHT_DCS_KERNEL");
-  return v;
-}
-
 /* ====================================== several chains in one launch (§8f.4)
  * Block b of a chains launch serves chain b % K as its block b / K of nblk
  * (the bodies take their block index and count), staging that chain's
@@ -1819,7 +1752,7 @@ __global__ void __launch_bounds__(kBlock) mhrs_finish_chains(const SweepArgs *ar
   const SweepArgs &a = args[blockIdx.x % (unsigned)K];
   const unsigned blk = blockIdx.x / (unsigned)K;
   if ((long)blk * kClaimChunk >= a.count) return; /* the whole block: its chain has fewer observations */
-  sweep_body<NT, kMethodMHRS, false, EnvPrivate, true>(a, blk, nblk); /* persistent (mhrs_finish_kernel) */
+  mhrs_finish_body<NT, false>(a, blk, nblk); /* persistent (mhrs_finish_kernel) */
 }
 
 /* h: the chains' arguments on the host (sizing), d: the same K SweepArgs on
@@ -1944,25 +1877,11 @@ static hipError_t launch_nt(const SweepArgs &a, int method, bool debug, hipStrea
     if (hipError_t e = launch_mhrs_search<NT>(a, st); e != hipSuccess) return e;
     return debug ? launch_mhrs_finish<NT, true>(a, st) : launch_mhrs_finish<NT, false>(a, st);
   } else if (method == kMethodDCS) {
-    if (dcs_legacy()) {
-#ifdef PHT_LEGACY_KERNELS
-      return debug ? launch_persist<NT, kMethodDCS, true>(a, st) : launch_persist<NT, kMethodDCS, false>(a, st);
-#else
-      return hipErrorNotSupported;
-#endif
-    }
     return debug ? launch_dcs_round<NT, true>(a, st) : launch_dcs_round<NT, false>(a, st);
   } else {
     /* ECS censored observations: the host always launches them as their own
      * range (allcens), concurrently with the exact range */
     if (!a.allcens) return hipErrorInvalidValue;
-    if (cens_legacy()) {
-#ifdef PHT_LEGACY_KERNELS
-      return debug ? launch_persist<NT, kMethodECS, true>(a, st) : launch_persist<NT, kMethodECS, false>(a, st);
-#else
-      return hipErrorNotSupported;
-#endif
-    }
     return debug ? launch_cens_round<NT, true>(a, st) : launch_cens_round<NT, false>(a, st);
   }
   return hipGetLastError();
