@@ -433,6 +433,12 @@ struct pht_ctx {
   int rccl_cap = 0;
   bool stats_zero = false;   /* d_stats zeroed on `stream` after the last sweep's copy */
   hipEvent_t evd = nullptr;  /* the statistics copy to the host is done */
+  /* the statistics block published by pht_stats_out_kernel: host-pinned
+   * coherent words + a flag the host polls (nullptr: the copy + event path,
+   * or PHT_STATS_COPY=1) */
+  unsigned long long *h_out = nullptr, *d_out = nullptr;
+  unsigned *h_flag = nullptr, *d_flag = nullptr;
+  unsigned seq = 0;
 };
 
 /* lanes of the persistent ECS grid on an MI355X (256 CUs x 2 blocks x 256) */
@@ -896,6 +902,24 @@ extern "C" pht_ctx *pht_ctx_create(int device, int n, int method, int mhit) {
     delete c;
     return nullptr;
   }
+  /* the published statistics (optional: without them the copy + event path) */
+  if (!getenv("PHT_STATS_COPY")) {
+    void *ho = nullptr, *hf = nullptr, *dout = nullptr, *dflag = nullptr;
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+    if (hipHostMalloc(&ho, sizeof(unsigned long long) * stats_len(n), fl) == hipSuccess &&
+        hipHostMalloc(&hf, 64, fl) == hipSuccess && hipHostGetDevicePointer(&dout, ho, 0) == hipSuccess &&
+        hipHostGetDevicePointer(&dflag, hf, 0) == hipSuccess) {
+      c->h_out = static_cast<unsigned long long *>(ho);
+      c->d_out = static_cast<unsigned long long *>(dout);
+      c->h_flag = static_cast<unsigned *>(hf);
+      c->d_flag = static_cast<unsigned *>(dflag);
+      *c->h_flag = 0u;
+    } else {
+      if (ho) (void)hipHostFree(ho);
+      if (hf) (void)hipHostFree(hf);
+      (void)hipGetLastError();
+    }
+  }
   return c;
 }
 
@@ -913,6 +937,8 @@ extern "C" void pht_ctx_destroy(pht_ctx *c) {
   if (c->evf) (void)hipEventDestroy(c->evf);
   if (c->evj) (void)hipEventDestroy(c->evj);
   if (c->evd) (void)hipEventDestroy(c->evd);
+  if (c->h_out) (void)hipHostFree(c->h_out);
+  if (c->h_flag) (void)hipHostFree(c->h_flag);
   if (c->comm) rccl_destroy(c->comm);
   if (c->d_rccl) (void)hipFree(c->d_rccl);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
@@ -1237,17 +1263,61 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
       return -1;
     }
   }
-  HIPCHK(hipMemcpyAsync(c->h_stats, c->d_stats, sizeof(unsigned long long) * sl, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipEventRecord(c->evd, c->stream)); /* ctx_wait waits for this, not for the zeroing */
-  HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * sl, c->stream));
+  if (c->h_out) {
+    /* one small kernel publishes the block and zeroes it; ctx_wait polls the
+     * flag (kernel end -> host sees the statistics: the blit copy's dispatch,
+     * its copy and the event's completion signal replaced by one dispatch and
+     * a store over the link; profiles/r05/stats_out/) */
+    if (++c->seq == 0u) c->seq = 1u;
+    HIPCHK(pht_launch_stats_out(c->d_stats, c->d_out, c->d_flag, c->seq, sl, c->stream));
+  } else {
+    HIPCHK(hipMemcpyAsync(c->h_stats, c->d_stats, sizeof(unsigned long long) * sl, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipEventRecord(c->evd, c->stream)); /* ctx_wait waits for this, not for the zeroing */
+    HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * sl, c->stream));
+  }
   c->stats_zero = true;
   return 0;
 }
 
+/* the flag pht_stats_out_kernel sets for this sweep; the stream is queried
+ * now and then, so a failed or finished-without-flag sweep ends the wait */
+static int wait_stats_flag(pht_ctx *c) {
+  for (unsigned long spin = 1;; spin++) {
+    if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == c->seq) return 0;
+    if ((spin & 1023ul) == 0ul) {
+      const hipError_t e = hipStreamQuery(c->stream);
+      if (e == hipSuccess) {
+        if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == c->seq) return 0;
+        set_err("device %d: the sweep finished without publishing its statistics", c->device);
+        return -1;
+      }
+      if (e != hipErrorNotReady) {
+        set_err("device %d: %s", c->device, hipGetErrorString(e));
+        return -1;
+      }
+    }
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+  }
+}
+
 static int ctx_wait(pht_ctx *c) {
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipEventSynchronize(c->evd));
-  HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  if (c->h_out) {
+    if (wait_stats_flag(c)) return -1;
+    memcpy(c->h_stats, c->h_out, sizeof(unsigned long long) * stats_len(c->n));
+    /* ev1 precedes the publishing kernel on the stream: it has completed */
+    hipError_t e = hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+    if (e == hipErrorNotReady) {
+      HIPCHK(hipEventSynchronize(c->ev1));
+      e = hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+    }
+    HIPCHK(e);
+  } else {
+    HIPCHK(hipEventSynchronize(c->evd));
+    HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  }
   if (c->method == kMethodMHRS && c->d_mcnt && getenv("PHT_MHRS_COUNTS")) {
     /* diagnostics: tasks still unresolved after MHRS search rounds 0..4 */
     unsigned q[5];

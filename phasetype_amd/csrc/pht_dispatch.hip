@@ -23,6 +23,30 @@ PHT_DECL(15)
 PHT_DECL(20)
 #undef PHT_DECL
 
+/* The sweep's statistics block to the host without a copy engine round trip
+ * (ctx_enqueue, gibbs_host.cpp): one workgroup reads the block, stores it
+ * into host-pinned coherent memory and zeroes it for the next sweep; after
+ * a system-scope fence of every thread, thread 0 publishes seq in the
+ * host-visible flag with a release store.  The host polls that flag instead
+ * of waiting on an event behind a blit copy and a fill. */
+__global__ void __launch_bounds__(256) pht_stats_out_kernel(unsigned long long *d, unsigned long long *h,
+                                                            unsigned *flag, unsigned seq, int sl) {
+  for (int k = threadIdx.x; k < sl; k += blockDim.x) {
+    h[k] = d[k];
+    d[k] = 0ull;
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" hipError_t pht_launch_stats_out(unsigned long long *d_stats, unsigned long long *h_out_dev,
+                                           unsigned *flag_dev, unsigned seq, int sl, hipStream_t st) {
+  if (sl < 1 || !d_stats || !h_out_dev || !flag_dev) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pht_stats_out_kernel, dim3(1), dim3(256), 0, st, d_stats, h_out_dev, flag_dev, seq, sl);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t pht_launch_sweep(const pht::SweepArgs *a, int method, int debug, hipStream_t st) {
   using namespace pht;
   if (a->n < 1 || a->n > kMaxN) return hipErrorInvalidValue;
