@@ -260,3 +260,29 @@ def test_fixed_point_overflow_is_an_error(gpu, method):
     with pytest.raises(P.PhaseTypeError, match="overflowed int64"):
         sw.gibbs(3, method, nu, zeta, T, Cm, P.zexp_for(y2))
     sw.close()
+
+
+@pytest.mark.parametrize("method", [2, 1, 4])
+def test_published_statistics_equal_the_copy_path(gpu, monkeypatch, method):
+    """The statistics block reaches the host through pht_stats_out_kernel
+    (host-pinned words + a polled flag, gibbs_host.cpp ctx_wait) by default;
+    PHT_STATS_COPY=1 (read at context creation) takes the copy + event path.
+    Several sweeps of a 30 % censored shard: the same block every sweep (the
+    published block is also zeroed for the next sweep by the same kernel)."""
+    n = 5
+    S, s = bd_exit(n)
+    y, cen = simulate_ph(S, s, 3000, seed=11, censor_frac=0.3)
+    zexp = P.zexp_for(y)
+    out = {}
+    for mode in ("pub", "copy"):
+        if mode == "copy":
+            monkeypatch.setenv("PHT_STATS_COPY", "1")
+        else:
+            monkeypatch.delenv("PHT_STATS_COPY", raising=False)
+        sw = P.Sweeper(n, method, 1)
+        sw.set_obs(y, cen)
+        out[mode] = [sw.sweep(S, s, key=(7, 9), sweep=k, zexp=zexp).copy() for k in range(1, 5)]
+        sw.close()
+    for a, b in zip(out["pub"], out["copy"]):
+        assert np.array_equal(a, b)
+    assert not np.array_equal(out["pub"][0], out["pub"][1])  # different sweeps, different draws
