@@ -752,7 +752,7 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
   unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
 #ifdef PHT_ECS_DIAG
   unsigned c_big = 0, c_wbig = 0, c_wround = 0, c_act = 0;
-  unsigned c_start = 0, c_pend = 0, c_new = 0, c_wnew = 0, c_wpend = 0;
+  unsigned c_start = 0, c_pend = 0, c_new = 0, c_wnew = 0, c_wpend = 0, c_w13 = 0;
 #endif
   for (;;) {
     bool need = false;
@@ -878,7 +878,11 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
       c_pend += pend ? 1u : 0u;
       c_new += (nnew > 0) ? 1u : 0u;
       const bool wnew = __any(nnew > 0), wpend = __any(pend);
+      /* the converged blocks run at 13 points this round (a pending lane
+       * with 11 points before its insert) */
+      const bool w13 = __any(pend && !bigl && env.cnt + 2 > 11);
       if ((threadIdx.x & 63) == 0) {
+        c_w13 += w13 ? 1u : 0u;
         c_wbig += __any(bigl) ? 1u : 0u;
         c_wround++;
         c_wnew += wnew ? 1u : 0u;
@@ -936,6 +940,7 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
   lds_add(&xc[12], (unsigned long long)c_new);
   lds_add(&xc[13], (unsigned long long)c_wnew);
   lds_add(&xc[14], (unsigned long long)c_wpend);
+  lds_add(&xc[5], (unsigned long long)c_w13);
 #endif
   __syncthreads();
   flush_stats(a.stats, zq, Bc, Nc, xc, n);

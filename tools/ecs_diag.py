@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """ECS round diagnostics from a -D PHT_ECS_DIAG variant build (PHT_LIB):
 how often lanes run the general ARMS code (envelope beyond the converged
-round's 13 points) and how many wave-rounds that divergence touches.
+round's 13 points) and how many wave-rounds that divergence touches, and
+the width the converged blocks run at (9, 11 or 13 points: the widest
+envelope in the wavefront; word 5 counts the 13-point wave-rounds).
 usage (GPU box): PHT_LIB=phasetype_amd/_variants/diag.so python3 tools/ecs_diag.py [--n 10 --N 1000000]"""
 import argparse
 import json
@@ -31,6 +33,9 @@ print(json.dumps({"n": a.n, "N": a.N, "kernel_ms": sw.last_kernel_ms(), "obs": i
                   "lane_rounds_active": int(ex[9]), "lane_rounds_start": int(ex[10]),
                   "lane_rounds_pend": int(ex[11]), "lane_rounds_newobs": int(ex[12]),
                   "wave_rounds_with_newobs": int(ex[13]), "wave_rounds_with_pend": int(ex[14]),
+                  "wave_rounds_cap13": int(ex[5]),
+                  "frac_wave_rounds_cap13": float(ex[5]) / max(1.0, float(ex[8])),
+                  "frac_wave_rounds_cap11": float(ex[14] - ex[5]) / max(1.0, float(ex[8])),
                   "active_lane_frac": float(ex[9]) / max(1.0, 64.0 * float(ex[8])),
                   "frac_wave_rounds_with_big": float(ex[7]) / max(1.0, float(ex[8])),
                   "big_per_jump": float(ex[6]) / max(1.0, float(ex[4]))}))
