@@ -23,6 +23,8 @@ CASES = [
     (15, 600, 0.3, 2, 1), (15, 300, 0.3, 1, 1), (15, 300, 0.3, 4, 1),
     # n = 20 censored ECS: the censored kernel's 9-point LDS envelope and its private continuation
     (20, 600, 0.5, 2, 1),
+    # the compile-time n = 20 MHRS and DCS kernels (n = 32 in test_gpu_edges.py runs the runtime-n ones)
+    (20, 300, 0.3, 1, 1), (20, 300, 0.3, 4, 1),
 ]
 
 
