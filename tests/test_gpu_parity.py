@@ -333,7 +333,9 @@ def test_row_kernel_longest_paths(gpu, orc, monkeypatch, n):
 
 @pytest.mark.parametrize("launch", ["one", "streams"])
 @pytest.mark.parametrize("method,n,cf", [(2, 5, 0.3), (2, 10, 0.0), (1, 3, 0.3), (4, 3, 0.0), (8, 6, 0.3),
-                                         (1, 10, 0.3), (4, 10, 0.0)])
+                                         (1, 10, 0.3), (4, 10, 0.0),
+                                         # the compile-time n = 15 / 20 chains kernels (cfg5 / cfg3 shapes)
+                                         (2, 15, 0.3), (1, 15, 0.3), (4, 15, 0.3), (2, 20, 0.0)])
 def test_chains_equal_single_runs(gpu, method, n, cf, launch, monkeypatch):
     """pht_gibbs_run_chains (independent chains on their own contexts,
     streams and host threads): chain c is bit-identical to
