@@ -116,18 +116,19 @@ def test_time_scale(gpu, orc, method, scale):
     assert 2.0 ** -zexp < 1e-14 * y.sum()
 
 
-@pytest.mark.parametrize("method", [1, 2])
-def test_all_censored(gpu, orc, method):
-    S, s = bd_exit(6)
+@pytest.mark.parametrize("method,n", [(1, 6), (2, 6), (2, 15), (1, 15)])
+def test_all_censored(gpu, orc, method, n):
+    """(n = 15: the compile-time censored kernel alone, no exact range)"""
+    S, s = bd_exit(n)
     y, _ = simulate_ph(S, s, 500, seed=77)
-    _check(orc, 6, method, y, np.ones(len(y), np.int32))
+    _check(orc, n, method, y, np.ones(len(y), np.int32))
 
 
-@pytest.mark.parametrize("mhit", [0, 3])
-def test_mhrs_mhit(gpu, orc, mhit):
-    S, s = bd_exit(4)
+@pytest.mark.parametrize("mhit,n", [(0, 4), (3, 4), (3, 10)])
+def test_mhrs_mhit(gpu, orc, mhit, n):
+    S, s = bd_exit(n)
     y, cen = simulate_ph(S, s, 400, seed=31 + mhit, censor_frac=0.2)
-    _check(orc, 4, 1, y, cen, mhit=mhit)
+    _check(orc, n, 1, y, cen, mhit=mhit)
 
 
 def test_mhrs_single_hard_observation(gpu, orc):

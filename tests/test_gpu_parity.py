@@ -68,7 +68,7 @@ def test_per_observation_bitexact(gpu, orc, n, N, cf, method, mhit):
     assert np.array_equal(st[:2 * n + n * n], g["stats"][:2 * n + n * n])
 
 
-@pytest.mark.parametrize("n,N,cf", [(3, 2000, 0.0), (10, 1000, 0.3), (15, 300, 0.0)])
+@pytest.mark.parametrize("n,N,cf", [(3, 2000, 0.0), (10, 1000, 0.3), (15, 300, 0.0), (20, 300, 0.3)])
 def test_dcs_brent_root_bitexact(gpu, orc, monkeypatch, n, N, cf):
     """PHT_DCS_ROOT=brent: the jump times by Find02's Brent search (the
     reference's root finder) instead of the default Halley iteration, GPU vs
@@ -100,7 +100,7 @@ def test_dcs_brent_root_bitexact(gpu, orc, monkeypatch, n, N, cf):
     assert P.split_stats(h["stats"], n)[3][5] * 2 < P.split_stats(g["stats"], n)[3][5]
 
 
-@pytest.mark.parametrize("n,N,cf", [(3, 2000, 0.3), (10, 1000, 0.0), (15, 300, 0.3)])
+@pytest.mark.parametrize("n,N,cf", [(3, 2000, 0.3), (10, 1000, 0.0), (15, 300, 0.3), (20, 300, 0.0)])
 def test_dcs_end_state_prepass_bitexact(gpu, orc, monkeypatch, n, N, cf):
     """PHT_DCS_PREPASS=1: the end states from the pre-pass kernel
     (dcs_end_kernel; by default only from 100k observations per shard) give
