@@ -1071,7 +1071,10 @@ static long exact_rowk(const pht_ctx *c) {
    * max over the 8 real shards 0.487 ms at 2,048, 0.508 at 1,024, 0.498 at
    * 4,096, 0.517 at 512 */
   if (c->n_exact * 10 <= 12 * L) return 2048;
-  if (c->n_exact <= 2 * L) return 1024;      /* 250k (r02): 0.57 ms (4,096: 0.59; none: 0.62) */
+  /* the 4-GPU shards of cfg4 (250k each; r05 kernels, profiles/r05/shards_curve/): slowest shard
+   * 0.621 / 0.621 / 0.630 ms at 4,096 against 0.641 / 0.627 / 0.641 at 1,024 (r02's kernels
+   * preferred 1,024: 0.57 vs 0.59 ms) */
+  if (c->n_exact <= 2 * L) return 4096;
   if (c->n_exact <= 5 * L) return 128;       /* cfg5's 350k exact: +5 % */
   return 0;                                  /* cfg4's 10^6: rows cost the one-lane range more (K = 64: +1 %) */
 }
