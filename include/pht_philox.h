@@ -98,7 +98,15 @@ PHT_HD2 pht_u32x4 pht_stream_block(pht_stream *s) {
 #if defined(__HIP_DEVICE_COMPILE__)
   /* every stream a wavefront holds carries its launch's key (SweepArgs k0/k1,
    * one per workgroup): read it as a wave-uniform value, so that the key
-   * schedule runs on the scalar unit and the rounds' xors take it from SGPRs */
+   * schedule runs on the scalar unit and the rounds' xors take it from SGPRs.
+   * INVARIANT (every pht_stream_init call site in phasetype_amd/csrc passes
+   * a.k0 / a.k1 of the block's own SweepArgs; ecs_chains_kernel and the
+   * *_chains kernels select one SweepArgs per block): all lanes of a wave
+   * use ONE key.  A kernel that mixed keys within a wave would get other
+   * lanes' streams here; tests/test_gpu_parity.py's chains tests (a
+   * different key per chain, chains interleaved block by block) are the
+   * guard, and tests/test_host.py checks that no call site takes its key
+   * from anything but SweepArgs. */
   return pht_philox4x32_10(c, __builtin_amdgcn_readfirstlane(s->k0), __builtin_amdgcn_readfirstlane(s->k1));
 #else
   return pht_philox4x32_10(c, s->k0, s->k1);

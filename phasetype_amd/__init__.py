@@ -54,6 +54,18 @@ EXPORTS = [
 ]
 
 
+def lib_sha256() -> str:
+    """sha256 of the loaded libPhaseType.so (bench.py keys its PMC counters
+    on it: counters measured on another build are not reported)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    with open(load()._pht_path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
 def _lapack_path():
     env = os.environ.get("PHT_LAPACK_LIB")
     if env:
@@ -80,6 +92,7 @@ def load(build_if_needed: bool = True) -> C.CDLL:
     if not os.path.exists(path):
         raise PhaseTypeError(f"native library missing: {path} (run phasetype_amd/build.py)")
     L = C.CDLL(path, mode=C.RTLD_LOCAL)
+    L._pht_path = os.path.abspath(path)
     L.pht_last_error.restype = C.c_char_p
     L.pht_bind_lapack.argtypes = [C.c_char_p, C.c_char_p]
     L.pht_set_seed.argtypes = [C.c_uint32]

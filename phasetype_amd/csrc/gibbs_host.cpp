@@ -27,7 +27,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sched.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <condition_variable>
 #include <mutex>
@@ -409,11 +412,6 @@ struct pht_ctx {
   double *d_utab = nullptr;              /* UNIF per-sweep table (pht_unif.h) */
   long utab_cap = 0;                     /* its capacity in doubles */
   int *d_dcsb = nullptr;                 /* DCS: per-position end states (dcs_end_kernel) */
-  /* ECS hand-off records (strong-scaling regime, SweepArgs::hand) */
-  EcsCont *d_cbuf = nullptr;
-  unsigned *d_cready = nullptr, *d_cq = nullptr;
-  long cont_cap = 0;
-  unsigned cepoch = 0;
   /* debug buffers */
   long long *d_zq = nullptr;
   int *d_N = nullptr, *d_B = nullptr, *d_pre = nullptr, *d_flags = nullptr;
@@ -658,12 +656,6 @@ static void ctx_free_obs(pht_ctx *c) {
   c->utab_cap = 0;
   if (c->d_dcsb) (void)hipFree(c->d_dcsb);
   c->d_dcsb = nullptr;
-  if (c->d_cbuf) (void)hipFree(c->d_cbuf);
-  if (c->d_cready) (void)hipFree(c->d_cready);
-  if (c->d_cq) (void)hipFree(c->d_cq);
-  c->d_cbuf = nullptr;
-  c->d_cready = c->d_cq = nullptr;
-  c->cont_cap = 0;
   c->d_y = nullptr; c->d_cens = nullptr; c->d_gid = nullptr;
   c->d_mbest = c->d_mq0 = c->d_mq1 = nullptr;
   c->d_mcnt = nullptr;
@@ -770,8 +762,11 @@ extern "C" int pht_ctx_rccl_prepare(pht_ctx *c, int max_len) {
       set_err("pht_ctx_rccl_prepare: no device memory for %d words", max_len);
       return -1;
     }
-    c->rccl_cap = max_len;
   }
+  /* the agreed word count of every later pht_ctx_rccl_allreduce (ranks
+   * prepare with the same max_len; a larger buffer kept from before is
+   * reduced only over these words) */
+  c->rccl_cap = max_len;
   return 0;
 }
 
@@ -799,11 +794,6 @@ extern "C" int pht_ctx_attach_rccl(pht_ctx *c, const unsigned char *id, int nran
   return 0;
 }
 
-#ifdef PHT_HANDOFF
-/* present only in -D PHT_HANDOFF variant builds (the hand-off tests look for it) */
-extern "C" int pht_variant_handoff(void) { return 1; }
-#endif
-
 /* in-place sum of a host int64 vector over the context's communicator, on its
  * stream (the same all-reduce a sweep runs on its statistics block): the
  * attach-time self-test of phasetype_amd/dist.py compares it with
@@ -816,11 +806,12 @@ extern "C" int pht_ctx_rccl_allreduce(pht_ctx *c, long long *buf, int len) {
     set_err("pht_ctx_rccl_allreduce: need a context with an RCCL communicator");
     return -1;
   }
-  /* a bad length on this rank alone must not leave the peers inside the
-   * collective: it still enters it, with the prepared size clamped (zeros
-   * where it has no data), and reports the error afterwards */
+  /* every rank reduces exactly the prepared word count (the same on every
+   * rank, pht_ctx_rccl_prepare), whatever len it was given: a bad length on
+   * one rank alone then still matches its peers' collective (its words are
+   * zeros), and the error is reported afterwards */
   const bool badlen = !buf || len < 1 || len > c->rccl_cap;
-  const int nred = badlen ? std::max(1, std::min(len, c->rccl_cap)) : len;
+  const int nred = c->rccl_cap;
   (void)hipSetDevice(c->device);
   hipError_t e = hipMemsetAsync(c->d_rccl, 0, sizeof(long long) * nred, c->stream);
   if (e == hipSuccess && !badlen)
@@ -1033,18 +1024,6 @@ extern "C" int pht_ctx_set_obs(pht_ctx *c, const double *y, const int *cens, lon
     const bool pre = e ? atoi(e) != 0 : count >= kDcsPrepassMin;
     if (c->method == kMethodDCS && pre) HIPCHK(hipMalloc(&c->d_dcsb, sizeof(int) * count));
   }
-#ifdef PHT_HANDOFF
-  /* ECS hand-off records (a -D PHT_HANDOFF variant build only, when PHT_HAND
-   * asks for it): one per exact observation at most (each is handed off at
-   * most once) */
-  if (c->method == kMethodECS && c->n_exact > 0 && getenv("PHT_HAND") && atoi(getenv("PHT_HAND")) > 0) {
-    HIPCHK(hipMalloc(&c->d_cbuf, sizeof(EcsCont) * c->n_exact));
-    HIPCHK(hipMalloc(&c->d_cready, sizeof(unsigned) * c->n_exact));
-    HIPCHK(hipMalloc(&c->d_cq, sizeof(unsigned) * kContQ));
-    HIPCHK(hipMemset(c->d_cready, 0, sizeof(unsigned) * c->n_exact));
-    c->cont_cap = c->n_exact;
-  }
-#endif
   return 0;
 }
 
@@ -1074,22 +1053,9 @@ static long exact_rowk(const pht_ctx *c) {
   /* the 4-GPU shards of cfg4 (250k each; r05 kernels, profiles/r05/shards_curve/): slowest shard
    * 0.621 / 0.621 / 0.630 ms at 4,096 against 0.641 / 0.627 / 0.641 at 1,024 (r02's kernels
    * preferred 1,024: 0.57 vs 0.59 ms) */
-  if (c->n_exact <= 2 * L) return 4096;
+  if (c->n_exact <= 2 * L) return c->n == 10 ? 4096 : 1024; /* measured at n = 10 only: elsewhere r04's 1,024 */
   if (c->n_exact <= 5 * L) return 128;       /* cfg5's 350k exact: +5 % */
   return 0;                                  /* cfg4's 10^6: rows cost the one-lane range more (K = 64: +1 %) */
-}
-
-/* ECS hand-off threshold (SweepArgs::hand): with rows in the launch, a
- * one-lane path still running after this many jumps continues on a row.
- * PHT_HAND=k forces it (0 = off) */
-static int exact_hand(const pht_ctx *c) {
-#ifndef PHT_HANDOFF
-  (void)c;
-  return 0; /* the experimental hand-off exists only in -D PHT_HANDOFF variant builds */
-#endif
-  if (!c->d_cbuf) return 0;
-  if (const char *e = getenv("PHT_HAND")) return std::max(0, atoi(e));
-  return 0;
 }
 
 /* UNIF: size (and grow) the context's table for this sweep's parameters
@@ -1144,17 +1110,6 @@ static int ctx_launch(pht_ctx *c, const SweepArgs &a, bool debug) {
     ae.occ = exact_occ(c);
     ae.rowk = exact_rowk(c);
     ae.rowprio = getenv("PHT_ROWPRIO") ? atoi(getenv("PHT_ROWPRIO")) : 3;
-    ae.hand = ae.rowk > 0 ? exact_hand(c) : 0;
-    if (ae.hand > 0) {
-      ae.cbuf = c->d_cbuf;
-      ae.cready = c->d_cready;
-      ae.cq = c->d_cq;
-      ae.ccap = c->cont_cap;
-      if (++c->cepoch == 0) c->cepoch = 1; /* a record is current when its flag holds this launch's epoch */
-      ae.cepoch = c->cepoch;
-      ae.contblk = getenv("PHT_HANDBLK") ? atoi(getenv("PHT_HANDBLK")) : 128;
-      HIPCHK(hipMemsetAsync(c->d_cq, 0, sizeof(unsigned) * kContQ, c->stream));
-    }
     /* lane-major first claims when the shard is within ~2 observations per
      * lane (the longest paths, one per wavefront; tools/latency.py:
      * -10 % at 31k-125k per GPU); PHT_SPREAD=0|1 forces it */
@@ -1284,9 +1239,23 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
 
 /* the flag pht_stats_out_kernel sets for this sweep; the stream is queried
  * now and then, so a failed or finished-without-flag sweep ends the wait */
+/* host threads inside wait_stats_flag right now: with more than one (several
+ * chains driven from several threads, pht_gibbs_run_chains) a waiter yields
+ * its core to the others' host work instead of pausing on it */
+static std::atomic<int> g_stat_waiters{0};
+
+static int wait_stats_flag_spin(pht_ctx *c);
 static int wait_stats_flag(pht_ctx *c) {
+  g_stat_waiters.fetch_add(1, std::memory_order_relaxed);
+  const int rc = wait_stats_flag_spin(c);
+  g_stat_waiters.fetch_sub(1, std::memory_order_relaxed);
+  return rc;
+}
+
+static int wait_stats_flag_spin(pht_ctx *c) {
   for (unsigned long spin = 1;; spin++) {
     if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == c->seq) return 0;
+    if (g_stat_waiters.load(std::memory_order_relaxed) > 1) sched_yield();
     if ((spin & 1023ul) == 0ul) {
       const hipError_t e = hipStreamQuery(c->stream);
       if (e == hipSuccess) {

@@ -26,22 +26,6 @@ constexpr int kUnifMaxK = 2047; /* last row index (LDS: 3 (K+1) doubles per bloc
 constexpr double kUnifMaxLam = 1300.0; /* w_0 = 2^-1000 keeps every Poisson weight finite below this */
 constexpr long unif_tab_doubles(int n, int K) { return 4 + 3L * (K + 1) + (long)(K + 1) * n; }
 
-/* ECS exact, strong-scaling regime (pht_kernels_impl.h, "hand-off"): a
- * one-lane path still running after SweepArgs::hand jumps is written out at
- * a jump boundary and continued on a 16-lane row of the same launch.  The
- * record is the path's whole state there: the next draw's stream position,
- * the remaining time, the state, E0 = e^{lambda_i yt} and the next absorb
- * test's denominator, and the observation's counters. */
-struct EcsCont {
-  long pos;
-  double yt;
-  int j, njump;
-  int flags, neval, lnjump, pad;
-  pht_stream r;
-  double E0[kMaxN];
-};
-constexpr int kContQ = 4; /* queue words: records allocated, claimed by rows, one-lane waves done, poll overruns */
-
 struct SweepArgs {
   const unsigned char *params; /* packed block (pht_layout.h), device */
   int n;
@@ -65,15 +49,6 @@ struct SweepArgs {
                                   blocks (both set by the launcher) */
   int nmain;
   int rowprio;                 /* ECS exact: wave priority of the row blocks (s_setprio 0-3) */
-  int hand;                    /* ECS exact with rows: a one-lane path still running after `hand` jumps moves to a
-                                  row of the same launch (0 = off); the records: */
-  EcsCont *cbuf;               /* [ccap] */
-  unsigned *cready;            /* [ccap] the launch epoch once record i is written */
-  unsigned *cq;                /* [kContQ], zeroed per launch */
-  long ccap;
-  unsigned cepoch;             /* this launch's epoch (never 0) */
-  int contblk;                 /* blocks of the launch whose rows continue handed-off paths (set by the launcher
-                                  from the host's request in this field) */
   int dcsbrent;                /* DCS: jump times by Find02's Brent search instead of hob_halley (pht_dcs_round.h) */
   int *dcsb;                   /* DCS: per position the end state (| flag), written by dcs_end_kernel ahead of
                                   the round kernel; nullptr: computed in the round kernel */

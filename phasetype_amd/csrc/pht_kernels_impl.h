@@ -93,9 +93,11 @@ struct Sink {
     if (DEBUG) *dpre = j;
   }
   /* DEBUG instantiations: a round in the general ARMS code, and whether its
-   * envelope reached private memory (kXDbgGeneral, kXDbgPrivate) */
+   * envelope reached private memory (kXDbgGeneral, kXDbgPrivate).  Not in
+   * PHT_STAMPS or PHT_ECS_DIAG builds, whose extra words 8 / 9 carry their
+   * own counters (stamps; wave-rounds and active lane-rounds) */
   __device__ __forceinline__ void arms_diag(bool general, bool priv) {
-#ifndef PHT_STAMPS
+#if !defined(PHT_STAMPS) && !defined(PHT_ECS_DIAG)
     if constexpr (DEBUG) {
       if (general) lds_add(&xc[kXDbgGeneral], 1ull);
       if (priv) lds_add(&xc[kXDbgPrivate], 1ull);
@@ -653,9 +655,8 @@ __device__ __forceinline__ void stage_ecs_params(const SweepArgs &a, PHT_LDS uns
 #define PHT_ECS_WAVES 0
 #endif
 /* blk / nblk: the block's index and the block count of its chain's grid
- * (blockIdx.x / gridDim.x, except in ecs_chains_kernel).  HAND: the launch
- * has row blocks that continue the paths this body hands off (a.hand) */
-template <int NT, bool DEBUG, bool HAND = false>
+ * (blockIdx.x / gridDim.x, except in ecs_chains_kernel) */
+template <int NT, bool DEBUG>
 __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = nval<NT>(a.n);
@@ -795,41 +796,6 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
         need = true;
         break;
       }
-      if constexpr (HAND) {
-        /* hand-off (strong-scaling regime): a path still running after
-         * a.hand jumps goes, at this jump boundary (its absorb test next),
-         * to a 16-lane row of the same launch (ecs_row_body), which
-         * continues it with the same draws and arithmetic; the lane takes
-         * its next observation */
-        if (a.hand > 0 && st.njump >= a.hand && st.haveE0) {
-          const unsigned idx = atomicAdd(&a.cq[0], 1u);
-          if (idx < (unsigned long)a.ccap) {
-            EcsCont *c = a.cbuf + idx;
-            /* (the next absorb test's denominator is not carried: the row
-             * recomputes it, the same pht_dot16 of the same vectors) */
-            if (DEBUG) c->pos = pos; /* (only the per-observation outputs need it: no live range otherwise) */
-            c->yt = st.yt;
-            c->j = st.j;
-            c->njump = st.njump;
-            c->flags = ln.flags;
-            c->neval = ln.neval;
-            c->lnjump = ln.njump;
-            c->r = ln.r;
-#pragma unroll
-            for (int i = 0; i < PHT_VEC(NT); i++)
-              if (i < n) c->E0[i] = st.E0[i];
-#ifdef PHT_TRACE_HAND
-            if (idx < 3)
-              printf("P idx=%u pos=%ld yt=%.17g j=%d nj=%d blk=%u na=%d nb=%d E0=%.17g fl=%d\n", idx, pos, st.yt, st.j,
-                     st.njump, ln.r.blk, ln.r.na, ln.r.nb, st.E0[0], ln.flags);
-#endif
-            __threadfence();
-            __hip_atomic_store(&a.cready[idx], a.cepoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            have = false;
-            continue;
-          }
-        }
-      }
       if (ecs_try_absorb(P, ln, sk, st)) {
         const uint32_t nd = pht_stream_pos(&ln.r);
         if (DEBUG) {
@@ -908,14 +874,6 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
       have = false;
     }
   }
-  if constexpr (HAND) {
-    /* this wave hands off no more paths: the rows stop waiting for records
-     * once every one-lane wave has said so and the queue is drained */
-    if (a.hand > 0 && (threadIdx.x & 63) == 0) {
-      __threadfence();
-      atomicAdd(&a.cq[2], 1u);
-    }
-  }
 #ifdef PHT_STAMPS
   /* diagnostic builds: the extra words carry [rounds, 15 stamp slots] */
   (void)c_obs; (void)c_neval; (void)c_flag; (void)c_nd; (void)c_jump;
@@ -953,7 +911,7 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
  * The row waves issue at raised priority: they carry the sweep's critical
  * path while one-lane blocks share their CUs.
  */
-template <int NT, bool DEBUG, bool CONT = false>
+template <int NT, bool DEBUG>
 __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, unsigned nblk) {
   extern __shared__ __align__(16) unsigned char smem[];
   constexpr int n = NT;
@@ -995,18 +953,6 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
   bool pend = false, bigm = false;
   long pos = 0;
   bool have = false, done = false;
-  /* hand-off (a.hand > 0): once its static positions are taken, a row claims
-   * the next continuation record (queue slot cidx) and polls for it once per
-   * round, never blocking the wave's other rows; it leaves when every
-   * one-lane wave is done and no record is left for it */
-  /* continuation rows: per row in LDS, [0] waiting for record [1], [2]
-   * polls so far */
-  __shared__ unsigned rowq[kBlock / kRowW][3];
-  const int rq = (int)(threadIdx.x / kRowW);
-  if (CONT && id.lead) {
-    rowq[rq][0] = 0u;
-    rowq[rq][2] = 0u;
-  }
   unsigned c_obs = 0, c_neval = 0, c_flag = 0, c_nd = 0, c_jump = 0;
   /* the path of the row is complete (its statistics recorded) */
   auto complete = [&]() {
@@ -1034,110 +980,34 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
     if (have && !pend) pht_stream_topup(&ln.r);
     while (!done && !pend) {
       if (!have) {
-        if constexpr (CONT) {
-          /* continuation rows (hand-off): claim the next record, then poll
-           * for it once per round, never blocking the wave's other rows;
-           * leave when every one-lane wave is done and no record is left */
-          /* rowq is read and written by the row's lead lane only and
-           * broadcast with __shfl: a plain LDS read by the other lanes would
-           * race with the lead's store (the compiler may keep an old value) */
-          unsigned cidx = 0;
-          if (id.lead) {
-            if (!rowq[rq][0]) {
-              rowq[rq][1] = atomicAdd(&a.cq[1], 1u);
-              rowq[rq][0] = 1u;
-            }
-            cidx = rowq[rq][1];
-          }
-          cidx = (unsigned)__shfl((int)cidx, 0, kRowW);
-          const unsigned nwaves_main = (unsigned)a.nmain * (kBlock / 64);
-          unsigned e = 0, dn = 0, al = 0;
-          const bool inb = cidx < (unsigned long)a.ccap;
-          if (id.lead) {
-            if (inb) e = __hip_atomic_load(&a.cready[cidx], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            dn = __hip_atomic_load(&a.cq[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            al = __hip_atomic_load(&a.cq[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          e = (unsigned)__shfl((int)e, 0, kRowW);
-          dn = (unsigned)__shfl((int)dn, 0, kRowW);
-          al = (unsigned)__shfl((int)al, 0, kRowW);
-          if (inb && e == a.cepoch) {
-            /* the path's state at its jump boundary: its absorb test is next
-             * (the denominator is recomputed: the same pht_dot16).  Every lane
-             * orders its reads of the record after the lead's observation of
-             * the flag (agent-scope acquire: invalidates this CU's L1) */
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            const EcsCont *c = a.cbuf + cidx;
-            if (DEBUG) pos = c->pos;
-            ln.r = c->r;
-            ln.flags = c->flags;
-            ln.neval = c->neval;
-            ln.nbrent = 0;
-            ln.njump = c->lnjump;
-            st.yt = c->yt;
-            st.j = c->j;
-            st.njump = c->njump;
-            st.haveE0 = true;
-            st.haveDen = false;
-            st.fold = false;
-#pragma unroll
-            for (int h = 0; h < RowV<NT>::H; h++) st.E0.v[h] = id.sv[h] ? c->E0[id.ix[h]] : 0.0;
-            if (DEBUG) {
-              sk.dz = a.dbg_zq + pos * n;
-              sk.dN = a.dbg_N + pos * n * n;
-              sk.dB = a.dbg_B + pos;
-              sk.dpre = a.dbg_pre + pos;
-            }
-            if (id.lead) rowq[rq][0] = 0u;
-            have = true;
-#ifdef PHT_TRACE_HAND
-            if (cidx < 3 && id.rl < 2)
-              printf("C cidx=%u rl=%d pos=%ld yt=%.17g j=%d nj=%d blk=%u na=%d nb=%d E0v0=%.17g fl=%d\n", cidx, id.rl, pos,
-                     st.yt, st.j, st.njump, ln.r.blk, ln.r.na, ln.r.nb, st.E0.v[0], ln.flags);
-#endif
-          } else if (!inb || (dn >= nwaves_main && cidx >= al)) {
-            done = true;
-            break;
-          } else {
-            unsigned np = 0;
-            if (id.lead) np = ++rowq[rq][2];
-            np = (unsigned)__shfl((int)np, 0, kRowW);
-            if (np > (1u << 22)) { /* never: the records come within the launch */
-              if (id.lead) atomicAdd(&a.cq[3], 1u);
-              done = true;
-            }
-            break; /* idle this round */
-          }
-        } else {
-          int t = 0;
-          if (id.lead) t = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          t = __shfl(t, 0, kRowW);
-          const long p = (long)t * nblk + blk;
-          if (p >= a.rowk) {
-            done = true;
-            break;
-          }
-          pos = a.begin - a.rowk + p; /* the rows' positions precede the launch range */
-          pht_stream_init(&ln.r, a.k0, a.k1, a.gid[pos], 0u, a.sweep);
-          ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
-          if (DEBUG) {
-            sk.dz = a.dbg_zq + pos * n;
-            sk.dN = a.dbg_N + pos * n * n;
-            sk.dB = a.dbg_B + pos;
-            sk.dpre = a.dbg_pre + pos;
-          }
-          /* ecs_begin */
-          const double target = dev_u(ln.r);
-          const int B = pistart(P, target, ln.flags);
-          if (id.lead) sk.start(B);
-          st.yt = a.y[pos];
-          st.j = B;
-          st.njump = 0;
-          st.haveE0 = false;
-          st.haveDen = false;
-          st.fold = false;
-          have = true;
+        int t = 0;
+        if (id.lead) t = __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        t = __shfl(t, 0, kRowW);
+        const long p = (long)t * nblk + blk;
+        if (p >= a.rowk) {
+          done = true;
+          break;
         }
+        pos = a.begin - a.rowk + p; /* the rows' positions precede the launch range */
+        pht_stream_init(&ln.r, a.k0, a.k1, a.gid[pos], 0u, a.sweep);
+        ln.flags = 0; ln.neval = 0; ln.nbrent = 0; ln.njump = 0;
+        if (DEBUG) {
+          sk.dz = a.dbg_zq + pos * n;
+          sk.dN = a.dbg_N + pos * n * n;
+          sk.dB = a.dbg_B + pos;
+          sk.dpre = a.dbg_pre + pos;
+        }
+        /* ecs_begin */
+        const double target = dev_u(ln.r);
+        const int B = pistart(P, target, ln.flags);
+        if (id.lead) sk.start(B);
+        st.yt = a.y[pos];
+        st.j = B;
+        st.njump = 0;
+        st.haveE0 = false;
+        st.haveDen = false;
+        st.fold = false;
+        have = true;
       }
       /* after a jump the absorb test runs inside the round (row_round) */
       if (!st.fold && row_try_absorb<NT>(P, id, ln, sk, st)) {
@@ -1154,15 +1024,7 @@ __device__ __forceinline__ void ecs_row_body(const SweepArgs &a, unsigned blk, u
 #endif
     if (need || pend) pht_stream_topup(&ln.r);
     PHT_STAMP(ln, 12);
-    if constexpr (CONT) {
-      if (__any(need) || __any(pend)) {
-        if (row_round<NT>(P, id, ln, ev, benv, sk, st, need, pend, bigm, pd)) complete();
-      } else {
-        __builtin_amdgcn_s_sleep(8); /* every row of the wave waits for a record */
-      }
-    } else {
-      if (row_round<NT>(P, id, ln, ev, benv, sk, st, need, pend, bigm, pd)) complete();
-    }
+    if (row_round<NT>(P, id, ln, ev, benv, sk, st, need, pend, bigm, pd)) complete();
   }
 #ifdef PHT_STAMPS
   (void)c_obs; (void)c_neval; (void)c_flag; (void)c_nd; (void)c_jump;
@@ -1197,7 +1059,7 @@ template <int NT, bool ROWS = false>
 constexpr int ecs_waves() {
   return PHT_ECS_WAVES > 0 ? PHT_ECS_WAVES : ((NT == 15 || NT == 20 || (ROWS && NT == 10)) ? 2 : 1);
 }
-template <int NT, bool DEBUG, bool ROWS, bool HAND = false>
+template <int NT, bool DEBUG, bool ROWS>
 __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(DEBUG ? 1 : ecs_waves<NT, ROWS>())))
 ecs_exact_kernel(SweepArgs a) {
@@ -1213,22 +1075,10 @@ ecs_exact_kernel(SweepArgs a) {
       ecs_row_body<NT, DEBUG>(a, blockIdx.x, (unsigned)a.rowblk);
       return;
     }
-    /* HAND (its own instantiation, so the kernels without it keep their
-     * register allocation): the one-lane blocks hand off their long paths;
-     * ecs_cont_kernel continues them after this launch */
-    ecs_exact_body<NT, DEBUG, HAND>(a, blockIdx.x - (unsigned)a.rowblk, (unsigned)a.nmain);
+    ecs_exact_body<NT, DEBUG>(a, blockIdx.x - (unsigned)a.rowblk, (unsigned)a.nmain);
   } else {
     ecs_exact_body<NT, DEBUG>(a, blockIdx.x, gridDim.x);
   }
-}
-
-/* the hand-off's continuation launch: rows take the records the one-lane
- * blocks of the launch before wrote (all complete), until none is left */
-template <int NT, bool DEBUG>
-__global__ void __launch_bounds__(kBlock)
-__attribute__((amdgpu_waves_per_eu(DEBUG ? 1 : ecs_waves<NT, true>())))
-ecs_cont_kernel(SweepArgs a) {
-  ecs_row_body<NT, DEBUG, true>(a, blockIdx.x, gridDim.x);
 }
 
 /*
@@ -1255,22 +1105,13 @@ static int smem_bytes_ecs(int n) {
 
 template <int NT, bool DEBUG>
 static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
-  static LaunchCfg cfg, cfgr, cfgh;
+  static LaunchCfg cfg, cfgr;
   const int sm = smem_bytes_ecs<NT>(a.n);
   const bool rows = row_ok<NT>() && a.rowk > 0;
-#ifdef PHT_HANDOFF
-  const bool hand = rows && a.hand > 0;
-  const void *kfn = hand   ? (const void *)ecs_exact_kernel<NT, DEBUG, row_ok<NT>(), true>
-                    : rows ? (const void *)ecs_exact_kernel<NT, DEBUG, row_ok<NT>()>
-                           : (const void *)ecs_exact_kernel<NT, DEBUG, false>;
-#else
-  /* (the experimental hand-off kernels exist only in -D PHT_HANDOFF builds) */
-  const bool hand = false;
   const void *kfn = rows ? (const void *)ecs_exact_kernel<NT, DEBUG, row_ok<NT>()>
                          : (const void *)ecs_exact_kernel<NT, DEBUG, false>;
-#endif
   int occ = 0, cus = 0;
-  if (hipError_t e = launch_config(hand ? cfgh : (rows ? cfgr : cfg), kfn, sm, &occ, &cus); e != hipSuccess)
+  if (hipError_t e = launch_config(rows ? cfgr : cfg, kfn, sm, &occ, &cus); e != hipSuccess)
     return e;
   /* the rowk longest observations on 16-lane rows (kBlock / kRowW per
    * block), ahead of the one-lane blocks in the same launch */
@@ -1290,9 +1131,6 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
     rk -= kRows;
   b.rowk = std::max(0L, rk);
   b.rowblk = (int)((b.rowk + (kBlock / kRowW) - 1) / (kBlock / kRowW));
-  if (b.rowblk == 0 || !rows || !hand) b.hand = 0; /* hand-off needs rows to take the paths */
-  /* continuation launch (hand-off): its blocks, after the main launch */
-  b.contblk = (b.hand > 0) ? (int)std::max(1L, std::min((long)a.contblk, slots)) : 0;
   b.begin = a.begin + b.rowk;
   b.count = a.count - b.rowk;
   const long want = (b.count + kBlock - 1) / kBlock;
@@ -1301,14 +1139,6 @@ static hipError_t launch_ecs_exact(const SweepArgs &a, hipStream_t st) {
   if (grid < 0) grid = 0;
   b.nmain = (int)grid;
   if (grid + b.rowblk < 1) return hipSuccess;
-#ifdef PHT_HANDOFF
-  if (rows && b.hand > 0) {
-    hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG, row_ok<NT>(), true>), dim3((unsigned)(grid + b.rowblk)),
-                       dim3(kBlock), sm, st, b);
-    if constexpr (row_ok<NT>())
-      hipLaunchKernelGGL((ecs_cont_kernel<NT, DEBUG>), dim3((unsigned)b.contblk), dim3(kBlock), sm, st, b);
-  } else
-#endif
   if (rows)
     hipLaunchKernelGGL((ecs_exact_kernel<NT, DEBUG, row_ok<NT>()>), dim3((unsigned)(grid + b.rowblk)), dim3(kBlock), sm,
                        st, b);

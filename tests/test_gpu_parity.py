@@ -557,67 +557,3 @@ def _oracle_chain_zexp(orc, it, mhit, method, n, nu, zeta, T, Cm, y, cen, zexp):
     their data); the oracle's LJMA_Gibbs would take its own from y."""
     return orc.gibbs_zexp(1, it, mhit, method, n, nu, zeta, T.reshape(-1, order="F"), Cm.reshape(-1, order="F"), y,
                           cen, zexp)
-
-
-
-
-# ---------------------------------------------- ECS hand-off (strong scaling)
-# Experimental, measured slower (DESIGN.md §7): only a -D PHT_HANDOFF variant
-# build has it (tools/build_variant.py -D PHT_HANDOFF; PHT_LIB=<that build>).
-def _has_handoff():
-    return hasattr(P.load(), "pht_variant_handoff")
-
-
-handoff_only = pytest.mark.skipif("not _has_handoff()", reason="the default library carries no hand-off kernels "
-                                  "(a -D PHT_HANDOFF variant build does)")
-
-
-@pytest.mark.parametrize("n,N,cf,hand", [(10, 20000, 0.0, 3), (10, 30000, 0.3, 8), (3, 20000, 0.0, 2),
-                                         (5, 20000, 0.3, 4), (15, 8000, 0.0, 3), (20, 6000, 0.0, 5)])
-@handoff_only
-def test_handoff_bitexact(gpu, orc, monkeypatch, n, N, cf, hand):
-    """PHT_HAND=k: one-lane paths still running after k jumps are written out
-    at a jump boundary and continued on 16-lane rows of the same launch
-    (pht_kernels_impl.h).  Per observation (start state, pre-absorption
-    state, flags, draws, fixed-point z, N) identical to the oracle's device
-    spec, and the product launch's totals to the per-observation launch."""
-    monkeypatch.setenv("PHT_HAND", str(hand))
-    monkeypatch.setenv("PHT_HANDBLK", "8")
-    S0, s0 = bd_exit(n)
-    y, cen = simulate_ph(S0, s0, N, seed=7000 + n, censor_frac=cf)
-    S, s = _perturbed(n, n + 11)
-    key, sweep = (0x71 + n, 0x5), 3
-    zexp = int(orc.lib.orc_zexp(np.ascontiguousarray(y), len(y)))
-    o = orc.dev_sweep(2, S, s, y, cen, key=key, sweep=sweep, zexp=zexp)
-    sw = P.Sweeper(n, 2, 1)
-    sw.set_obs(y, cen)
-    g = sw.sweep_debug(S, s, key=key, sweep=sweep, zexp=zexp)
-    for f in ("B", "pre", "flags", "ndraw"):
-        bad = np.nonzero(g[f] != o[f])[0]
-        assert bad.size == 0, f"{f} differs at obs {bad[:5]}: gpu {g[f][bad[:5]]} oracle {o[f][bad[:5]]}"
-    assert np.array_equal(g["zq"], o["zq"]) and np.array_equal(g["N"], o["N"])
-    st = sw.sweep(S, s, key=key, sweep=sweep, zexp=zexp)
-    sw.close()
-    assert np.array_equal(st[:2 * n + n * n], g["stats"][:2 * n + n * n])
-    assert P.split_stats(st, n)[3][0] == N
-
-
-@handoff_only
-def test_handoff_chain_unchanged(gpu, monkeypatch):
-    """The Gibbs chain with hand-off equals the chain without it, bit for bit
-    (the 8-GPU shard size, n = 10)."""
-    n = 10
-    T, theta = bd_exit_structure(n)
-    S, s = bd_exit(n)
-    y, cen = simulate_ph(S, s, 125000, seed=8125)
-    m = len(theta)
-    nu, zeta, Cm = 1 + 50 * theta, np.full(m, 50.0), np.ones(T.shape)
-    out = {}
-    for hand in ("0", "20", "6"):
-        monkeypatch.setenv("PHT_HAND", hand)
-        sw = P.Sweeper(n, 2, 1)
-        sw.set_obs(y, cen)
-        P.set_seed(77)
-        out[hand] = sw.gibbs(6, 2, nu, zeta, T, Cm, P.zexp_for(y))
-        sw.close()
-    assert np.array_equal(out["0"], out["20"]) and np.array_equal(out["0"], out["6"])

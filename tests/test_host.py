@@ -387,3 +387,23 @@ def test_log_pos_equals_log_on_the_draws_domain(orc):
     orc.lib.orc_detlog_v(x.ctypes.data_as(C.c_void_p), a.ctypes.data_as(C.c_void_p), C.c_long(len(x)))
     orc.lib.orc_detlogpos_v(x.ctypes.data_as(C.c_void_p), b.ctypes.data_as(C.c_void_p), C.c_long(len(x)))
     assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+def test_philox_key_sources_are_launch_uniform():
+    """pht_stream_block reads the key through readfirstlane
+    (include/pht_philox.h), which is correct only when every lane of a wave
+    uses one key.  Every device call site must take the key from its block's
+    SweepArgs (a.k0, a.k1), the resident chain's ResidentArgs (r.k0, r.k1) or
+    a function parameter pair (k0, k1) that is itself fed from SweepArgs."""
+    import re
+
+    csrc = os.path.join(REPO, "phasetype_amd", "csrc")
+    sites = []
+    for f in sorted(os.listdir(csrc)):
+        if not f.endswith((".h", ".hip")):
+            continue
+        for m in re.finditer(r"pht_stream_init(?:_block0)?\(\s*[^,]+,\s*([^,]+),\s*([^,]+),", open(os.path.join(csrc, f)).read()):
+            sites.append((f, m.group(1).strip(), m.group(2).strip()))
+    assert len(sites) >= 10
+    for f, k0, k1 in sites:
+        assert (k0, k1) in {("a.k0", "a.k1"), ("r.k0", "r.k1"), ("k0", "k1")}, (f, k0, k1)
