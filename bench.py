@@ -75,7 +75,7 @@ def cpu_baseline(n, y, cen, T, nu, zeta, method=2, target_s=15.0):
                       f"single thread of the GPU box's host CPU"}
 
 
-def load_counters(path, n, n_local, method, lib_sha):
+def load_counters(path, n, n_local, method, lib_key):
     """PMC counters of profiles/traffic_latest.json for this workload, or
     (None, None, reason).  Fail closed: the file must name the sha256 of the
     library this process loaded (the counters were measured on that build)
@@ -87,9 +87,9 @@ def load_counters(path, n, n_local, method, lib_sha):
         tf = json.load(open(path))
     except Exception as e:  # noqa: BLE001
         return None, None, f"unreadable counter file: {e}"
-    if tf.get("lib_sha256") != lib_sha:
-        return None, None, (f"counters measured on library {str(tf.get('lib_sha256'))[:12]}, "
-                            f"this run loaded {lib_sha[:12]}: not reported")
+    if tf.get("lib_key") != lib_key:
+        return None, None, (f"counters measured on library {str(tf.get('lib_key'))[:16]}, "
+                            f"this run loaded {lib_key[:16]}: not reported")
     if (tf.get("n"), tf.get("N_local"), tf.get("method")) != (n, n_local, method):
         return None, None, "counters measured on another workload"
     return tf.get("hbm_bytes_per_launch"), tf.get("fp64_flops_per_launch"), f"PMC of this library: {tf.get('pmc_dir')}"
@@ -267,8 +267,8 @@ def main():
         sweeps_per_s = args.steps / dt
         local_obs = hi - lo
         achieved = ALG_BYTES_PER_OBS * local_obs / (kernel_ms * 1e-3) / 1e9
-        lib_sha = P.lib_sha256()
-        traffic, flops, traffic_src = load_counters(args.traffic_file, n, local_obs, args.method, lib_sha)
+        lib_key = P.lib_key()
+        traffic, flops, traffic_src = load_counters(args.traffic_file, n, local_obs, args.method, lib_key)
         line = {
             "metric": "Gibbs iterations/sec (whole node), n=10 states × N=1e6 observations",
             "value": sweeps_per_s,
@@ -287,7 +287,7 @@ def main():
                                    f"N={N} obs ({args.censor:.0%} censored), priors nu=1+50*theta, zeta=50, mhit=1",
                        "n": n, "N": N, "method": args.method, "parallelism": f"obs-shard x{world}",
                        "stats_reduce": reduce_note},
-            "lib_sha256": lib_sha,
+            "lib_key": lib_key,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kernel_ms, "traffic_source": traffic_src,

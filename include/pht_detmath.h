@@ -123,6 +123,9 @@ __shared__ double pht_lds_log_tab[768];
 #define PHT_LOG_TAB pht_log_tab
 #endif
 
+#ifndef PHT_EXP_ASMC
+#define PHT_EXP_ASMC(c) "v"(c)
+#endif
 #ifndef PHT_EXP_LOWK
 #define PHT_EXP_LOWK 1
 #endif
@@ -152,11 +155,23 @@ PHT_HD double pht_exp_core(double x) {
   const int idx = ki & 63;
   const int k = ki >> 6; /* floor(ki / 64) */
   const double sc = PHT_EXP_TAB[2 * idx], tail = PHT_EXP_TAB[2 * idx + 1];
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PHT_EXP_ASMFMA)
+  /* the same fmas as three-address v_fma_f64 (no v_fmac with a copied
+   * constant accumulator under register pressure) */
+  double q;
+  const double c6 = 1.3888888888888889419e-03, c5 = 8.3333333333333332177e-03, c4 = 4.1666666666666664354e-02,
+               c3 = 1.6666666666666665741e-01;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(q) : PHT_EXP_ASMC(c6), "v"(r), PHT_EXP_ASMC(c5));
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(q) : "v"(q), "v"(r), PHT_EXP_ASMC(c4));
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(q) : "v"(q), "v"(r), PHT_EXP_ASMC(c3));
+  q = fma(q, r, 0.5);
+#else
   double q = 1.3888888888888889419e-03;   /* 1/6! */
   q = fma(q, r, 8.3333333333333332177e-03); /* 1/5! */
   q = fma(q, r, 4.1666666666666664354e-02); /* 1/4! */
   q = fma(q, r, 1.6666666666666665741e-01); /* 1/3! */
   q = fma(q, r, 0.5);
+#endif
   const double p = fma(r * r, q, r); /* e^r - 1 */
   /* res * 2^k with one rounding (subnormal results) */
   return ldexp(sc + fma(sc, p, tail), k);

@@ -54,16 +54,22 @@ EXPORTS = [
 ]
 
 
-def lib_sha256() -> str:
-    """sha256 of the loaded libPhaseType.so (bench.py keys its PMC counters
-    on it: counters measured on another build are not reported)."""
+def lib_key() -> str:
+    """Identity of the loaded native library, which bench.py keys its PMC
+    counters on (counters measured on another build are not reported):
+    "src:<sha256 of the build inputs>" for the in-tree library (the same for
+    every build of those sources: the .so bytes embed the build directory),
+    "file:<sha256 of the file>" for a PHT_LIB variant."""
     import hashlib
 
+    path = load()._pht_path
+    if os.path.abspath(path) == os.path.abspath(_build.LIB) and "PHT_LIB" not in os.environ:
+        return "src:" + _build.source_key()
     h = hashlib.sha256()
-    with open(load()._pht_path, "rb") as f:
+    with open(path, "rb") as f:
         for chunk in iter(lambda: f.read(1 << 20), b""):
             h.update(chunk)
-    return h.hexdigest()
+    return "file:" + h.hexdigest()
 
 
 def _lapack_path():

@@ -43,15 +43,35 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+def inputs() -> list:
+    """Every file the default library is built from (sources, headers, this
+    script with its flags)."""
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps += [os.path.join(REPO, "include", f) for f in ("phasetype_amd.h", "pht_detmath.h", "pht_philox.h",
+                                                          "pht_gamma.h", "pht_eigen.h")]
+    deps.append(os.path.abspath(__file__))
+    return deps
+
+
+def source_key() -> str:
+    """sha256 over the default library's build inputs (name + content): the
+    same for every build of the same sources, wherever it was compiled (the
+    .so itself embeds its build directory)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for d in inputs():
+        h.update(os.path.relpath(d, REPO).encode() + b"\0")
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps += [os.path.join(REPO, "include", f) for f in ("phasetype_amd.h", "pht_detmath.h", "pht_philox.h",
-                                                          "pht_gamma.h", "pht_eigen.h")]
-    deps.append(__file__)
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    return any(os.path.getmtime(d) > t for d in inputs() if os.path.exists(d))
 
 
 def _merge_defines(defines) -> list:

@@ -153,8 +153,18 @@ struct Lane {
     (ln).st_acc[k] += t_ - (ln).st_last;                              \
     (ln).st_last = t_;                                                \
   } while (0)
+#elif defined(PHT_ISA_MARKS)
+/* static-analysis builds only (tools/isa_phases.py, never run): an assembly
+ * comment at each stamp site splits the kernel's ISA into the stamped phases */
+#define PHT_STAMP(ln, k) asm volatile("; @phase " #k)
+/* a wave-uniform variant inside a phase (e.g. the converged blocks' width),
+ * closed by PHT_ISA_SUB("end") */
+#define PHT_ISA_SUB(tag) asm volatile("; @sub " tag)
 #else
 #define PHT_STAMP(ln, k) do { } while (0)
+#endif
+#ifndef PHT_ISA_SUB
+#define PHT_ISA_SUB(tag) do { } while (0)
 #endif
 
 /* ===================================================================== ARMS */
@@ -585,12 +595,16 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
     const double x = y_t - d;
     double acc;
     if (haveE0 && d == 0.0) {
+      PHT_ISA_SUB("d0");
       acc = dev_dot16([&](int i) { return w(i); }, E0, n);
+      PHT_ISA_SUB("end");
     } else {
+      PHT_ISA_SUB("dx");
 #pragma unroll
       for (int i = 0; i < n; i++) Elast[i] = pht_exp_neg(P.evals(i) * x);
       acc = dev_dot16([&](int i) { return w(i); }, Elast, n);
       lastd = d;
+      PHT_ISA_SUB("end");
     }
     return pht_log(acc) + Sjj * d;
   }
@@ -633,6 +647,7 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
         acc[3] = fma(q, x3, m[0]);
       }
     } else {
+      PHT_ISA_SUB("rare");
       if (E0w && mk) {
 #pragma unroll
         for (int i = 0; i < n; i++) E0w[i] = pht_exp_neg(P.evals(i) * y_t);
@@ -644,6 +659,7 @@ struct EcsDens { /* log(sum_i W[j,i] e^{λ_i (y_t - d)}) + S_jj d */
         for (int i = 0; i < n; i++) T[i] = pht_exp_neg(P.evals(i) * (y_t - xinit[k]));
         acc[k] = dev_dot16(Wj, T, n);
       }
+      PHT_ISA_SUB("end");
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) yv[k] = pht_log(acc[k]) + Sjj * xinit[k];
@@ -740,6 +756,9 @@ __device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink 
   return fin;
 }
 
+#ifndef PHT_MM_ARRAY_NT
+#define PHT_MM_ARRAY_NT 15 /* the compile-time n whose moveMass keeps register arrays */
+#endif
 /* end of a non-absorbing jump once the sojourn d is drawn: moveMass +
  * categorical (:350-358), statistics (:362-363) */
 template <int NT, class Sink>
@@ -761,26 +780,30 @@ __device__ __forceinline__ void ecs_jump_finish(const Par<NT> &P, Lane &ln, Sink
 #pragma unroll
     for (int i = 0; i < n; i++) E[i] = f.Elast[i];
   } else {
+    PHT_ISA_SUB("rare");
 #pragma unroll
     for (int i = 0; i < n; i++) E[i] = pht_exp_neg(P.evals(i) * x);
+    PHT_ISA_SUB("end");
   }
   st.yt = x;
   st.haveE0 = true;
   const int cnt = P.nsuccP(j);
-  double w[PHT_VEC(NT)], accs[PHT_VEC(NT)];
-  double sum = 0.0;
-#pragma unroll
-  for (int q = 0; q < PHT_VEC(NT); q++) {
-    if (q < cnt) {
-      const int k = P.succP(j, q);
-      accs[q] = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
-      w[q] = P.P(j, k) * accs[q];
-      sum += w[q];
-    }
-  }
-  const double target = dev_u(ln.r) * sum;
   int nj;
-  {
+  if constexpr (NT == PHT_MM_ARRAY_NT) {
+    /* n = 15 keeps the register-array form: the scan below costs it two
+     * spilled VGPRs (tests/test_kernel_regs.py) */
+    double w[PHT_VEC(NT)], accs[PHT_VEC(NT)];
+    double sum = 0.0;
+#pragma unroll
+    for (int q = 0; q < PHT_VEC(NT); q++) {
+      if (q < cnt) {
+        const int k = P.succP(j, q);
+        accs[q] = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
+        w[q] = P.P(j, k) * accs[q];
+        sum += w[q];
+      }
+    }
+    const double target = dev_u(ln.r) * sum;
     double sofar = 0.0;
     int sel = -1;
 #pragma unroll
@@ -795,12 +818,67 @@ __device__ __forceinline__ void ecs_jump_finish(const Par<NT> &P, Lane &ln, Sink
       sel = cnt - 1;
     }
     nj = (cnt > 0) ? P.succP(j, sel) : 0;
-    /* the next absorb test's denominator: same dot product, same E */
     double dsel = 0.0;
 #pragma unroll
     for (int q = 0; q < PHT_VEC(NT); q++) dsel = (q == sel) ? accs[q] : dsel;
     st.den = dsel;
     st.haveDen = (cnt > 0);
+  } else {
+    /* weights w_q = P[j,k_q] (QQs[k_q,.] . E) over the successors, their sum,
+     * then the categorical scan (:352-358).  The first two successors' values
+     * are kept (every state of a birth-death chain has at most two); any
+     * further one is recomputed in the scan, the same expressions in the same
+     * order, so the result does not depend on how many are kept.  (A register
+     * array over all n possible successors cost ~100 moves per round at
+     * n = 10: its zero-fill and shuffles) */
+    double w0 = 0.0, w1 = 0.0, a0 = 0.0, a1 = 0.0;
+    double sum = 0.0;
+    for (int q = 0; q < cnt; q++) {
+      const int k = P.succP(j, q);
+      const double acc = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
+      const double wq = P.P(j, k) * acc;
+      if (q == 0) {
+        a0 = acc;
+        w0 = wq;
+      } else if (q == 1) {
+        a1 = acc;
+        w1 = wq;
+      }
+      sum += wq;
+    }
+    const double target = dev_u(ln.r) * sum;
+    {
+      double sofar = 0.0, dsel = 0.0;
+      int sel = -1;
+      for (int q = 0; q < cnt; q++) {
+        double wq, aq;
+        if (q == 0) {
+          wq = w0;
+          aq = a0;
+        } else if (q == 1) {
+          wq = w1;
+          aq = a1;
+        } else {
+          const int k = P.succP(j, q);
+          aq = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
+          wq = P.P(j, k) * aq;
+        }
+        sofar += wq;
+        dsel = aq; /* the selected one, or the last (scan end) */
+        if (!(sofar < target)) {
+          sel = q;
+          break;
+        }
+      }
+      if (sel < 0) {
+        ln.flags |= kFlagScanEnd;
+        sel = cnt - 1;
+      }
+      nj = (cnt > 0) ? P.succP(j, sel) : 0;
+      /* the next absorb test's denominator: same dot product, same E */
+      st.den = dsel;
+      st.haveDen = (cnt > 0);
+    }
   }
   sk.z(j, d);
   sk.N(j, nj);

@@ -261,13 +261,17 @@ __device__ __forceinline__ void round_insert(Env &e, const ArmsPend &pd, F &f, L
   };
   put(pd.px, pd.py);
   if (pd.px < (1. - kXEps) * xl + kXEps * xr) {
+    PHT_ISA_SUB("rare");
     const double xn = (1. - kXEps) * xl + kXEps * xr;
     put(xn, f(xn));
     ln.neval++;
+    PHT_ISA_SUB("end");
   } else if (pd.px > kXEps * xl + (1. - kXEps) * xr) {
+    PHT_ISA_SUB("rare");
     const double xn = kXEps * xl + (1. - kXEps) * xr;
     put(xn, f(xn));
     ln.neval++;
+    PHT_ISA_SUB("end");
   }
 }
 
@@ -340,7 +344,11 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
     } else {
       f.init4(xinit, yv, mk, st.E0);
     }
-    if (mk && fin) ecs_first_E0(P, y_t, lam, st.E0); /* rare: no envelope computed it */
+    if (mk && fin) { /* rare: no envelope computed it */
+      PHT_ISA_SUB("rare");
+      ecs_first_E0(P, y_t, lam, st.E0);
+      PHT_ISA_SUB("end");
+    }
     st.haveE0 = true;
     /* a new observation's first absorb test (ecs_try_absorb: the same draw
      * and arithmetic, after its E0 above) */
@@ -376,9 +384,13 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
   /* ---- pending lanes: the update that ends the rejected iteration */
   if (pend) big = (env.cnt + 2 > kRoundCap);
   if (__any(pend && !big && env.cnt > 9)) {
+    PHT_ISA_SUB("c13");
     if (pend && !big) round_insert<13, round_lds_only<NT>()>(env, pd, f, ln);
+    PHT_ISA_SUB("end");
   } else {
+    PHT_ISA_SUB("c11");
     if (pend && !big) round_insert<11, round_lds_only<NT>()>(env, pd, f, ln);
+    PHT_ISA_SUB("end");
   }
   PHT_STAMP(ln, 3);
   /* ---- converged: intersections and areas over the widest envelope in
@@ -387,15 +399,15 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
   const int cap = __any(arm && env.cnt > 11) ? 13 : (__any(arm && env.cnt > 9) ? 11 : 9);
   double cs[kRoundCap]; /* cumulative areas, cumulate -> invert */
   if (arm) {
-    if (cap == 9) round_meets<9>(env, env.cnt - 1);
-    else if (cap == 11) round_meets<11>(env, env.cnt - 1);
-    else round_meets<13>(env, env.cnt - 1);
+    if (cap == 9) { PHT_ISA_SUB("c9"); round_meets<9>(env, env.cnt - 1); PHT_ISA_SUB("end"); }
+    else if (cap == 11) { PHT_ISA_SUB("c11"); round_meets<11>(env, env.cnt - 1); PHT_ISA_SUB("end"); }
+    else { PHT_ISA_SUB("c13"); round_meets<13>(env, env.cnt - 1); PHT_ISA_SUB("end"); }
   }
   PHT_STAMP(ln, 4);
   if (arm) {
-    if (cap == 9) round_cumulate<9>(env, cs);
-    else if (cap == 11) round_cumulate<11>(env, cs);
-    else round_cumulate<13>(env, cs);
+    if (cap == 9) { PHT_ISA_SUB("c9"); round_cumulate<9>(env, cs); PHT_ISA_SUB("end"); }
+    else if (cap == 11) { PHT_ISA_SUB("c11"); round_cumulate<11>(env, cs); PHT_ISA_SUB("end"); }
+    else { PHT_ISA_SUB("c13"); round_cumulate<13>(env, cs); PHT_ISA_SUB("end"); }
   }
   PHT_STAMP(ln, 5);
   if (start && !fin) {
@@ -417,9 +429,9 @@ __device__ __forceinline__ void ecs_round(const Par<NT> &P, Lane &ln, Env &env, 
   if (itr) {
     const double pu = dev_u(ln.r);
     constexpr bool LD = round_lds_only<NT>();
-    if (cap == 9) round_invert<9, LD>(env, cs, pu, q);
-    else if (cap == 11) round_invert<11, LD>(env, cs, pu, q);
-    else round_invert<13, LD>(env, cs, pu, q);
+    if (cap == 9) { PHT_ISA_SUB("c9"); round_invert<9, LD>(env, cs, pu, q); PHT_ISA_SUB("end"); }
+    else if (cap == 11) { PHT_ISA_SUB("c11"); round_invert<11, LD>(env, cs, pu, q); PHT_ISA_SUB("end"); }
+    else { PHT_ISA_SUB("c13"); round_invert<13, LD>(env, cs, pu, q); PHT_ISA_SUB("end"); }
     const double u = dev_u(ln.r) * q.ey;
     yv = logshift(u, env.ymax);
   }

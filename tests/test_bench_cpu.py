@@ -33,13 +33,13 @@ def test_bench_help():
 def test_counters_fail_closed(tmp_path):
     """VERDICT r05 Weak 7: bench.py reports PMC traffic / FP64 flops only
     when profiles/traffic_latest.json was measured on the library this run
-    loaded (its sha256) and on the same workload; otherwise null."""
+    loaded (its source key, phasetype_amd.lib_key) and on the same workload; otherwise null."""
     sys.path.insert(0, REPO)
     import bench
 
     f = tmp_path / "t.json"
     rec = {"n": 10, "N_local": 1000000, "method": "ECS", "hbm_bytes_per_launch": 1.5e7,
-           "fp64_flops_per_launch": 1.1e10, "lib_sha256": "ab" * 32, "pmc_dir": "profiles/r06/x"}
+           "fp64_flops_per_launch": 1.1e10, "lib_key": "ab" * 32, "pmc_dir": "profiles/r06/x"}
     f.write_text(json.dumps(rec))
     t, fl, why = bench.load_counters(str(f), 10, 1000000, "ECS", "ab" * 32)
     assert (t, fl) == (1.5e7, 1.1e10) and "profiles/r06/x" in why
@@ -47,7 +47,7 @@ def test_counters_fail_closed(tmp_path):
     assert t is None and fl is None and "not reported" in why
     t, fl, _ = bench.load_counters(str(f), 10, 125000, "ECS", "ab" * 32)
     assert t is None and fl is None
-    del rec["lib_sha256"]
+    del rec["lib_key"]
     f.write_text(json.dumps(rec))
     assert bench.load_counters(str(f), 10, 1000000, "ECS", "ab" * 32)[:2] == (None, None)
     assert bench.load_counters(str(tmp_path / "missing.json"), 10, 1000000, "ECS", "ab" * 32)[:2] == (None, None)
@@ -56,4 +56,4 @@ def test_counters_fail_closed(tmp_path):
 def test_committed_counters_name_a_library():
     """The committed counter file carries the library hash and its PMC directory."""
     d = json.load(open(os.path.join(REPO, "profiles", "traffic_latest.json")))
-    assert len(d.get("lib_sha256") or "") == 64 and os.path.isdir(os.path.join(REPO, d["pmc_dir"]))
+    assert (d.get("lib_key") or "").startswith(("src:", "file:")) and os.path.isdir(os.path.join(REPO, d["pmc_dir"]))

@@ -11,6 +11,8 @@ ab_isolation/).  Each worker owns one library; the parent sends "run" in
 interleaved order and only one worker uses the GPU at a time.
 
 usage (GPU box): python3 tools/ab.py --libs a.so b.so ... [--rounds 5 --sweeps 10]
+A library may carry environment settings for its worker: "a.so@PHT_ECS_OCC=1,PHT_ROWK=0"
+(the same library twice with different knobs is two variants).
 Each variant runs the bench workload (BD-exit(n), N obs, ECS) as a Gibbs
 run of --sweeps sweeps per round; rounds interleave the variants.  Prints a
 JSON summary: per-variant median / min ms per sweep and kernel ms.
@@ -64,7 +66,14 @@ class Lib:
         return dt, kms.value, res
 
 
-def _worker(conn, path, n, method, y, cen):
+def _split(spec):
+    path, _, env = spec.partition("@")
+    return path, dict(kv.split("=", 1) for kv in env.split(",") if kv)
+
+
+def _worker(conn, spec, n, method, y, cen):
+    path, env = _split(spec)
+    os.environ.update(env)
     lb = Lib(path, n, method, y, cen)
     while True:
         msg = conn.recv()
@@ -122,7 +131,7 @@ def main():
                     print(json.dumps({"error": f"{p} draws differ from {a.libs[0]}"}))
             times[p].append(dt / a.sweeps * 1e3)
             kern[p].append(kms / a.sweeps)
-    out = {os.path.basename(p): {"ms_per_sweep_median": float(np.median(times[p])), "ms_min": float(np.min(times[p])),
+    out = {(os.path.basename(_split(p)[0]) + ("@" + p.partition("@")[2] if "@" in p else "")): {"ms_per_sweep_median": float(np.median(times[p])), "ms_min": float(np.min(times[p])),
                                  "kernel_ms_median": float(np.median(kern[p]))} for p in a.libs}
     print(json.dumps(out, indent=1))
     for lb, pr in zip(libs, procs):

@@ -59,7 +59,7 @@ def main(d, out=None, kernel_sub=os.environ.get("PMC_KERNEL", "ecs_exact_kernel"
 def write_traffic(res, bench, path, src, pmc_dir=None):
     """profiles/traffic_latest.json: read by bench.py as roofline.traffic when
     its workload matches (n, local N, method) AND the library it loads is the
-    one profiled (lib_sha256, from the profiled bench line); pmc_dir = the
+    one profiled (lib_key, from the profiled bench line); pmc_dir = the
     committed profiles/ directory holding these passes."""
     der = res["derived"]
     if "hbm_bytes_per_launch" not in der or not bench:
@@ -71,7 +71,7 @@ def write_traffic(res, bench, path, src, pmc_dir=None):
          "hbm_write_bytes": der.get("hbm_write_bytes"),
          "fp64_flops_per_launch": der.get("fp64_flops_per_launch"),
          "kernel": "pht::ecs_exact_kernel",
-         "lib_sha256": bench.get("lib_sha256"),
+         "lib_key": bench.get("lib_key"),
          "pmc_dir": pmc_dir or os.path.relpath(src, os.environ.get("GRAFT_REPO_ROOT", os.getcwd())),
          "method_note": "FETCH_SIZE x 2 (gfx950 wide-read correction) x 1024 + WRITE_SIZE x 1024, "
                         "per-dispatch averages from separate --pmc passes (MI355X_MICROARCH.md HBM)"}
