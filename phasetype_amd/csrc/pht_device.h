@@ -756,9 +756,6 @@ __device__ __forceinline__ bool ecs_try_absorb(const Par<NT> &P, Lane &ln, Sink 
   return fin;
 }
 
-#ifndef PHT_MM_ARRAY_NT
-#define PHT_MM_ARRAY_NT 15 /* the compile-time n whose moveMass keeps register arrays */
-#endif
 /* end of a non-absorbing jump once the sojourn d is drawn: moveMass +
  * categorical (:350-358), statistics (:362-363) */
 template <int NT, class Sink>
@@ -789,28 +786,51 @@ __device__ __forceinline__ void ecs_jump_finish(const Par<NT> &P, Lane &ln, Sink
   st.haveE0 = true;
   const int cnt = P.nsuccP(j);
   int nj;
-  if constexpr (NT == PHT_MM_ARRAY_NT) {
-    /* n = 15 keeps the register-array form: the scan below costs it two
-     * spilled VGPRs (tests/test_kernel_regs.py) */
-    double w[PHT_VEC(NT)], accs[PHT_VEC(NT)];
-    double sum = 0.0;
-#pragma unroll
-    for (int q = 0; q < PHT_VEC(NT); q++) {
-      if (q < cnt) {
-        const int k = P.succP(j, q);
-        accs[q] = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
-        w[q] = P.P(j, k) * accs[q];
-        sum += w[q];
-      }
+  /* weights w_q = P[j,k_q] (QQs[k_q,.] . E) over the successors, their sum,
+   * then the categorical scan (:352-358).  The first two successors' values
+   * are kept (every state of a birth-death chain has at most two); any
+   * further one is recomputed in the scan, the same expressions in the same
+   * order, so the result does not depend on how many are kept.  (Register
+   * arrays over all n possible successors cost ~100 moves per round at
+   * n = 10, their zero-fill and shuffles, and pushed n = 20 further into
+   * spills: cfg3 kernel -6.7 %, cfg5 -3.0 %, cfg4 -0.75 %) */
+  double w0 = 0.0, w1 = 0.0, a0 = 0.0, a1 = 0.0;
+  double sum = 0.0;
+  for (int q = 0; q < cnt; q++) {
+    const int k = P.succP(j, q);
+    const double acc = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
+    const double wq = P.P(j, k) * acc;
+    if (q == 0) {
+      a0 = acc;
+      w0 = wq;
+    } else if (q == 1) {
+      a1 = acc;
+      w1 = wq;
     }
-    const double target = dev_u(ln.r) * sum;
-    double sofar = 0.0;
+    sum += wq;
+  }
+  const double target = dev_u(ln.r) * sum;
+  {
+    double sofar = 0.0, dsel = 0.0;
     int sel = -1;
-#pragma unroll
-    for (int q = 0; q < PHT_VEC(NT); q++) {
-      if (q < cnt && sel < 0) {
-        sofar += w[q];
-        if (!(sofar < target)) sel = q;
+    for (int q = 0; q < cnt; q++) {
+      double wq, aq;
+      if (q == 0) {
+        wq = w0;
+        aq = a0;
+      } else if (q == 1) {
+        wq = w1;
+        aq = a1;
+      } else {
+        const int k = P.succP(j, q);
+        aq = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
+        wq = P.P(j, k) * aq;
+      }
+      sofar += wq;
+      dsel = aq; /* the selected one, or the last (scan end) */
+      if (!(sofar < target)) {
+        sel = q;
+        break;
       }
     }
     if (sel < 0) {
@@ -818,67 +838,9 @@ __device__ __forceinline__ void ecs_jump_finish(const Par<NT> &P, Lane &ln, Sink
       sel = cnt - 1;
     }
     nj = (cnt > 0) ? P.succP(j, sel) : 0;
-    double dsel = 0.0;
-#pragma unroll
-    for (int q = 0; q < PHT_VEC(NT); q++) dsel = (q == sel) ? accs[q] : dsel;
+    /* the next absorb test's denominator: same dot product, same E */
     st.den = dsel;
     st.haveDen = (cnt > 0);
-  } else {
-    /* weights w_q = P[j,k_q] (QQs[k_q,.] . E) over the successors, their sum,
-     * then the categorical scan (:352-358).  The first two successors' values
-     * are kept (every state of a birth-death chain has at most two); any
-     * further one is recomputed in the scan, the same expressions in the same
-     * order, so the result does not depend on how many are kept.  (A register
-     * array over all n possible successors cost ~100 moves per round at
-     * n = 10: its zero-fill and shuffles) */
-    double w0 = 0.0, w1 = 0.0, a0 = 0.0, a1 = 0.0;
-    double sum = 0.0;
-    for (int q = 0; q < cnt; q++) {
-      const int k = P.succP(j, q);
-      const double acc = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
-      const double wq = P.P(j, k) * acc;
-      if (q == 0) {
-        a0 = acc;
-        w0 = wq;
-      } else if (q == 1) {
-        a1 = acc;
-        w1 = wq;
-      }
-      sum += wq;
-    }
-    const double target = dev_u(ln.r) * sum;
-    {
-      double sofar = 0.0, dsel = 0.0;
-      int sel = -1;
-      for (int q = 0; q < cnt; q++) {
-        double wq, aq;
-        if (q == 0) {
-          wq = w0;
-          aq = a0;
-        } else if (q == 1) {
-          wq = w1;
-          aq = a1;
-        } else {
-          const int k = P.succP(j, q);
-          aq = dev_dot16([&](int i) { return P.QQs(k, i); }, E, n);
-          wq = P.P(j, k) * aq;
-        }
-        sofar += wq;
-        dsel = aq; /* the selected one, or the last (scan end) */
-        if (!(sofar < target)) {
-          sel = q;
-          break;
-        }
-      }
-      if (sel < 0) {
-        ln.flags |= kFlagScanEnd;
-        sel = cnt - 1;
-      }
-      nj = (cnt > 0) ? P.succP(j, sel) : 0;
-      /* the next absorb test's denominator: same dot product, same E */
-      st.den = dsel;
-      st.haveDen = (cnt > 0);
-    }
   }
   sk.z(j, d);
   sk.N(j, nj);

