@@ -232,20 +232,46 @@ struct OneBlasThread {
   }
 };
 
+/* LAPACK workspace and scratch of eigen() per n, per host thread: the
+ * workspace size is the reference's query result for that n (a pure function
+ * of n), asked once instead of twice per sweep */
+struct EigenWork {
+  int n = -1, lw = 0;
+  std::vector<double> A, evi, Ql, scl, rce, rcv, work;
+  std::vector<int> iwork, ipiv;
+};
+
 static int eigen(int n, const double *S, double *evals, double *Q, double *Qinv) {
   OneBlasThread one;
   char balanc = 'B', jobv = 'V', sense = 'B';
   int lwork = -1, info = 0, ilo, ihi, nn = n;
   double wq = 0, abnrm;
-  std::vector<double> A(n * n), evi(n), Ql(n * n), scl(n), rce(n), rcv(n);
-  std::vector<int> iwork(2 * n + 2), ipiv(n);
-  p_dgeevx(&balanc, &jobv, &jobv, &sense, &nn, A.data(), &nn, evals, evi.data(), Ql.data(), &nn, Q, &nn, &ilo,
-           &ihi, scl.data(), &abnrm, rce.data(), rcv.data(), &wq, &lwork, nullptr, &info, 1, 1, 1, 1);
-  int lw = (int)wq;
-  p_dgetri(&nn, nullptr, &nn, nullptr, &wq, &lwork, &info);
-  if ((int)wq > lw) lw = (int)wq;
-  std::vector<double> work(lw > 0 ? lw : 1);
-  memcpy(A.data(), S, sizeof(double) * n * n);
+  /* (a pointer: a thread_local object with a destructor left an undefined
+   * EigenWork::~EigenWork in the shared library; one per thread, kept) */
+  static thread_local EigenWork *ewp = nullptr;
+  if (!ewp) ewp = new EigenWork;
+  EigenWork &ew = *ewp;
+  if (ew.n != n) {
+    ew.A.assign(n * n, 0.0);
+    ew.evi.assign(n, 0.0);
+    ew.Ql.assign(n * n, 0.0);
+    ew.scl.assign(n, 0.0);
+    ew.rce.assign(n, 0.0);
+    ew.rcv.assign(n, 0.0);
+    ew.iwork.assign(2 * n + 2, 0);
+    ew.ipiv.assign(n, 0);
+    p_dgeevx(&balanc, &jobv, &jobv, &sense, &nn, ew.A.data(), &nn, evals, ew.evi.data(), ew.Ql.data(), &nn, Q, &nn,
+             &ilo, &ihi, ew.scl.data(), &abnrm, ew.rce.data(), ew.rcv.data(), &wq, &lwork, nullptr, &info, 1, 1, 1, 1);
+    int lw = (int)wq;
+    p_dgetri(&nn, nullptr, &nn, nullptr, &wq, &lwork, &info);
+    if ((int)wq > lw) lw = (int)wq;
+    ew.lw = lw > 0 ? lw : 1;
+    ew.work.assign(ew.lw, 0.0);
+    ew.n = n;
+  }
+  int lw = ew.lw;
+  double *A = ew.A.data(), *evi = ew.evi.data(), *work = ew.work.data();
+  memcpy(A, S, sizeof(double) * n * n);
   /* The reference asks for condition numbers too (sense 'B'); they come
    * from dtrsna AFTER the eigenvectors and feed nothing it uses, so the
    * sweep skips them (sense 'N', same workspace as the 'B' query: the
@@ -253,8 +279,8 @@ static int eigen(int n, const double *S, double *evals, double *Q, double *Qinv)
    * Q^-1 stay bit-identical, tests/test_host.py).  That is most of the
    * per-sweep host time at n = 10. */
   char sense_n = 'N', jobvl_n = 'N';
-  p_dgeevx(&balanc, &jobvl_n, &jobv, &sense_n, &nn, A.data(), &nn, evals, evi.data(), Ql.data(), &nn, Q, &nn, &ilo,
-           &ihi, scl.data(), &abnrm, rce.data(), rcv.data(), work.data(), &lw, iwork.data(), &info, 1, 1, 1, 1);
+  p_dgeevx(&balanc, &jobvl_n, &jobv, &sense_n, &nn, A, &nn, evals, evi, ew.Ql.data(), &nn, Q, &nn, &ilo,
+           &ihi, ew.scl.data(), &abnrm, ew.rce.data(), ew.rcv.data(), work, &lw, ew.iwork.data(), &info, 1, 1, 1, 1);
   if (info != 0) {
     say("Error (LJMA_eigen 01): failed LAPACK call, code=%d\n", info);
     return info;
@@ -262,14 +288,72 @@ static int eigen(int n, const double *S, double *evals, double *Q, double *Qinv)
   for (int i = 0; i < n; i++)
     if (evi[i] > 0) say("Error: imaginary part of eigenvalue %d found.\n", i + 1);
   memcpy(Qinv, Q, sizeof(double) * n * n);
-  p_dgetrf(&nn, &nn, Qinv, &nn, ipiv.data(), &info);
+  p_dgetrf(&nn, &nn, Qinv, &nn, ew.ipiv.data(), &info);
   if (info != 0) {
     say("Error (LJMA_inverse 01): failed LAPACK call, code=%d\n", info);
     return info;
   }
-  p_dgetri(&nn, Qinv, &nn, ipiv.data(), work.data(), &lw, &info);
+  p_dgetri(&nn, Qinv, &nn, ew.ipiv.data(), work, &lw, &info);
   if (info != 0) say("Error (LJMA_inverse 03): failed LAPACK call, code=%d\n", info);
   return info;
+}
+
+/* the device-mode spectral products of the packed block (explicit fma in
+ * oracle/pht_oracle.c:orc_sp_build's order).  x86-64: a copy compiled with
+ * hardware fma runs where the host has it (the baseline ISA's fma() is
+ * glibc's software routine: half of build_params' time at n = 20); both are
+ * correctly rounded, so the values are the same. */
+static inline __attribute__((always_inline)) void spectral_products_body(int n, const double *S, const double *s,
+                                                                         const double *P, const double *Q,
+                                                                         const double *Qs, const double *Q1,
+                                                                         double *d, const Layout &L) {
+  double rj[kMaxN];
+  for (int j = 0; j < n; j++) {
+    const double Sjj = S[j + j * n];
+    d[L.logs + j] = s[j] > 0.0 ? pht_log(s[j]) : 0.0;
+    d[L.scale + j] = 1.0 / -Sjj;
+    d[L.logscale + j] = pht_log(d[L.scale + j]);
+    for (int k = 0; k < n; k++) rj[k] = S[j + k * n] / (-Sjj); /* hoisted: same quotients */
+    for (int i = 0; i < n; i++) {
+      double w = 0.0, v = 0.0;
+      for (int k = 0; k < n; k++) {
+        if (k != j) w = fma(rj[k], Q[k + i * n], w);
+        v = fma(P[j + k * n], Q[k + i * n], v);
+      }
+      d[L.QQs + j + i * n] = Q[j + i * n] * Qs[i];
+      d[L.W + j + i * n] = w * Qs[i];
+      d[L.QQ1 + j + i * n] = Q[j + i * n] * Q1[i];
+      d[L.V + j + i * n] = v * Q1[i];
+    }
+  }
+  for (int i = 0; i < n; i++) {
+    double a = 0.0;
+    for (int k = 0; k < n; k++) a = fma(d[L.pi + k], Q[k + i * n], a);
+    d[L.piQ + i] = a;
+  }
+  for (int j = 0; j < n; j++) { /* ECS starting point y_t - a (pht_detmath.h pht_wmoments) */
+    double m[PHT_WMOM];
+    pht_wmoments(n, d + L.W + j, n, d + L.evals, m);
+    for (int k = 0; k < PHT_WMOM; k++) d[L.Wm + j + k * n] = m[k];
+  }
+}
+#if defined(__x86_64__)
+__attribute__((target("fma"))) static void spectral_products_fma(int n, const double *S, const double *s,
+                                                                 const double *P, const double *Q, const double *Qs,
+                                                                 const double *Q1, double *d, const Layout &L) {
+  spectral_products_body(n, S, s, P, Q, Qs, Q1, d, L);
+}
+#endif
+static void spectral_products(int n, const double *S, const double *s, const double *P, const double *Q,
+                              const double *Qs, const double *Q1, double *d, const Layout &L) {
+#if defined(__x86_64__)
+  static const bool hw_fma = __builtin_cpu_supports("fma");
+  if (hw_fma) {
+    spectral_products_fma(n, S, s, P, Q, Qs, Q1, d, L);
+    return;
+  }
+#endif
+  spectral_products_body(n, S, s, P, Q, Qs, Q1, d, L);
 }
 
 /* ======================================================== sweep parameters */
@@ -318,35 +402,7 @@ static int build_params(int n, const double *S, const double *s, int method, std
       }
     }
   }
-  std::vector<double> rj(n);
-  for (int j = 0; j < n; j++) {
-    const double Sjj = S[j + j * n];
-    d[L.logs + j] = s[j] > 0.0 ? pht_log(s[j]) : 0.0;
-    d[L.scale + j] = 1.0 / -Sjj;
-    d[L.logscale + j] = pht_log(d[L.scale + j]);
-    for (int k = 0; k < n; k++) rj[k] = S[j + k * n] / (-Sjj); /* hoisted: same quotients */
-    for (int i = 0; i < n; i++) {
-      double w = 0.0, v = 0.0;
-      for (int k = 0; k < n; k++) {
-        if (k != j) w = fma(rj[k], Q[k + i * n], w);
-        v = fma(P[j + k * n], Q[k + i * n], v);
-      }
-      d[L.QQs + j + i * n] = Q[j + i * n] * Qs[i];
-      d[L.W + j + i * n] = w * Qs[i];
-      d[L.QQ1 + j + i * n] = Q[j + i * n] * Q1[i];
-      d[L.V + j + i * n] = v * Q1[i];
-    }
-  }
-  for (int i = 0; i < n; i++) {
-    double a = 0.0;
-    for (int k = 0; k < n; k++) a = fma(d[L.pi + k], Q[k + i * n], a);
-    d[L.piQ + i] = a;
-  }
-  for (int j = 0; j < n; j++) { /* ECS starting point y_t - a (pht_detmath.h pht_wmoments) */
-    double m[PHT_WMOM];
-    pht_wmoments(n, d + L.W + j, n, d + L.evals, m);
-    for (int k = 0; k < PHT_WMOM; k++) d[L.Wm + j + k * n] = m[k];
-  }
+  spectral_products(n, S, s, P, Q, Qs.data(), Q1.data(), d, L);
   for (int j = 0; j < n; j++) {
     int a = 0, b = 0, c = 0;
     for (int k = 0; k < n; k++) {
