@@ -1,5 +1,14 @@
+#!/usr/bin/env python3
+"""Model of the ECS one-lane kernel's per-block work (CPU only): the cfg4
+observations sorted by decreasing y, 64-observation chunks given to 512
+blocks of 256 persistent lanes (rounds per observation ~ 1 + 2.33 y), each
+block's finish = its busiest lane.  Compares the static stripes
+(claim_pos), boustrophedon stripes, LPT over chunks and a per-stripe greedy
+assignment.  (r06: the model's 12.5 % block imbalance did not show on the
+GPU, profiles/r06/claim_order/.)"""
+import os
 import sys, heapq, numpy as np
-sys.path.insert(0,'/root/repo')
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from phasetype_amd.synth import DATA_KEY, bd_exit, simulate_ph
 S,s=bd_exit(10)
 y,c=simulate_ph(S,s,1_000_000,seed=DATA_KEY)
