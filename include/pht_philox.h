@@ -16,8 +16,11 @@
  * uniform  (one word w):    u = (2w+1) * 2^-33, exact, 0 < u < 1 — the
  *                           resolution of R's unif_rand (2^-32);
  * uniform53 (two words a,b): m = (a << 20) | (b >> 12) (52 bits),
- *                           u = (2m+1) * 2^-53 — used where the tail of
- *                           -log(u) matters (exponential sojourns).
+ *                           u = (2m+1) * 2^-53;
+ * exponential uniform:      one word a >= 2^24 -> uniform53(a, 2^31) (the
+ *                           centre of a's 2^-32 cell), else uniform53(a, b)
+ *                           with a second word: -log(u) keeps its tail
+ *                           (exponential sojourns, pht_next_uexp).
  */
 #ifndef PHT_PHILOX_H
 #define PHT_PHILOX_H
@@ -152,6 +155,19 @@ PHT_HD2 double pht_next_u53(pht_stream *s) {
   const uint32_t a = pht_next_w(s);
   const uint32_t b = pht_next_w(s);
   return pht_u01(a, b);
+}
+
+/* the uniform of an exponential draw E = -log(U) (device spec, r06): one
+ * word when that word is >= 2^24 (U >= 2^-8, probability 1 - 2^-8), U = the
+ * centre of the word's 2^-32 cell; below, a second word places U on
+ * pht_u01's 2^-52 grid, so the tail of -log U (E > 5.5) keeps the
+ * resolution of the two-word uniform.  Words per exponential 2 -> 1.004
+ * (the MHRS attempt search draws one per jump; until r05 every exponential
+ * took pht_next_u53's two words) */
+PHT_HD2 double pht_next_uexp(pht_stream *s) {
+  const uint32_t a = pht_next_w(s);
+  if (a >= (1u << 24)) return pht_u01(a, 1u << 31);
+  return pht_u01(a, pht_next_w(s));
 }
 
 /* reposition to word index pos (replay) */

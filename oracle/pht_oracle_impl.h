@@ -53,7 +53,7 @@ static inline double ORC_FN(runif)(ORC_FN(rng) *r, double a, double b) {
 }
 static inline double ORC_FN(rexp)(ORC_FN(rng) *r, double scale) {
   if (!isfinite(scale) || scale <= 0.0) return scale == 0.0 ? 0.0 : NAN;
-  return scale * -pht_log(pht_next_u53(r));
+  return scale * -pht_log(pht_next_uexp(r));
 }
 #define ORC_EXP pht_exp
 #define ORC_EXP_NEG pht_exp_neg   /* arguments <= 0: spectral sums, stay-past-y */

@@ -130,7 +130,7 @@ __device__ __forceinline__ double dev_runif(pht_stream &r, double a, double b) {
 }
 __device__ __forceinline__ double dev_rexp(pht_stream &r, double scale) {
   if (!isfinite(scale) || scale <= 0.0) return scale == 0.0 ? 0.0 : __builtin_nan("");
-  return scale * -pht_log_pos(pht_next_u53(&r)); /* the uniform is in [2^-53, 1): pht_log's value */
+  return scale * -pht_log_pos(pht_next_uexp(&r)); /* the uniform is in [2^-53, 1): pht_log's value */
 }
 
 /* Lane context: random stream, flags and counters of the current observation. */

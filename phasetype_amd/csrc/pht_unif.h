@@ -44,7 +44,7 @@
  *     and counts N[c,b].  Draws per step: U (time), U (state).
  *  3. Exact: absorbed from j* at y (N[j*,j*]++, the reference's diagonal
  *     convention).  Censored: from j* at y the chain runs forward
- *     (memoryless): sojourn Exp(-S_jj) (two words), Pfull categorical over
+ *     (memoryless): sojourn Exp(-S_jj) (pht_next_uexp: one word, rarely two), Pfull categorical over
  *     succPf (one word; an overrun takes the last candidate, flag 1), until
  *     absorption.
  * Draw order: U1 (k*), U2 (j*), [U time, U state] x k*, then the censored
