@@ -158,7 +158,15 @@ def main():
     in_lib = dist is not None and coll_dev != "cpu" and os.environ.get("PHT_STATS_REDUCE", "rccl") == "rccl"
     reduce = None
     reduce_note = "none"
-    if dist is not None:
+    # one rank has nothing to sum: under torchrun at world 1 the sweep runs
+    # without a collective (an RCCL all-reduce over one rank still costs
+    # ~50 us per sweep, profiles/r06/torchrun/); PHT_WORLD1_REDUCE=1 keeps it
+    use_coll = dist is not None and (world > 1 or os.environ.get("PHT_WORLD1_REDUCE", "0") == "1")
+    if not use_coll:
+        in_lib = False
+        if dist is not None:
+            reduce_note = "none (world 1)"
+    else:
         if in_lib and not attach_rccl(sw, dist, coll_dev):
             log("[bench] in-library RCCL all-reduce failed its self-test; using the host callback")
             in_lib = False
@@ -208,7 +216,7 @@ def main():
         sw3.set_obs(y[lo:hi], cen[lo:hi], obs0=lo)
         sw3.set_global_count(N)
         red3 = None
-        if dist is not None:
+        if use_coll:
             if in_lib:
                 if not attach_rccl(sw3, dist, coll_dev):
                     raise SystemExit("in-library RCCL all-reduce passed its self-test once, then failed it")
