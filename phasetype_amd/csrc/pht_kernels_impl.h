@@ -230,6 +230,7 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
   double y = 0.0;
   /* attempt state */
   bool inatt = false, fresh = false;
+  uint32_t lrec = 0xffffffffu; /* the current task's record as last read */
   pht_stream r;
   double t = 0.0;
   int j = 0, lastj = 0, nj = 0;
@@ -260,6 +261,7 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
         gid = a.gid[pos];
         k = 0;
         have = true;
+        lrec = 0xffffffffu;
       }
       if (k >= K) {
         have = false;
@@ -271,8 +273,11 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
        * success; with one lane per task (round 0) only this lane writes the
        * record, and it stops at its own success: no load needed */
       bool stop = att >= (uint32_t)kMhrsMaxAtt;
-      if constexpr (W > 1)
-        stop = stop || (__hip_atomic_load(&a.mbest[task], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 8) < att;
+      /* the task's record as this lane last read it (below, once per
+       * iteration): no global load on the refill path (r06: MHRS cfg4
+       * -1.7 %, cfg5 -1.5 %, profiles/r06/mhrs_lrec/); a record that moved
+       * since drops the attempt after its first jump instead */
+      if constexpr (W > 1) stop = stop || (lrec >> 8) < att;
       if (stop) {
         have = false;
         continue;
@@ -306,6 +311,7 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
     uint32_t rec = 0xffffffffu;
     if constexpr (W > 1) {
       if (inatt && !fresh) rec = __hip_atomic_load(&a.mbest[task], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (inatt && !fresh) lrec = rec;
     }
     if (inatt && fresh) { /* start state of the attempt */
       const double target = pht_next_u(&r);
