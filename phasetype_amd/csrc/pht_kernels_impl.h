@@ -210,6 +210,9 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
   extern __shared__ __align__(16) unsigned char smem[];
   const int T1 = 1 + a.mhit;
   const long total = (qin ? (long)(*cin) : a.count * T1) * W;
+  /* round 0 zeroes the queue counters the later rounds' compactions add to
+   * (they run after it on the stream; no separate fill per sweep) */
+  if (qin == nullptr && blk == 0 && threadIdx.x < kMhrsCounters) a.mcnt[threadIdx.x] = 0u;
   /* block b owns claim chunks b, b + grid, ...: none when b * 64 >= total
    * (small shards, empty rounds): leave before staging anything */
   if ((long)blk * kClaimChunk >= total) return;
@@ -264,6 +267,10 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
         lrec = 0xffffffffu;
       }
       if (k >= K) {
+        /* round 0 (one lane per task, every task): no success in its K
+         * attempts -- this lane writes the task's record, so round 0 leaves
+         * every record defined and the sweep needs no fill of mbest */
+        if constexpr (W == 1) a.mbest[task] = kMhrsUnresolved;
         have = false;
         continue;
       }
@@ -1179,7 +1186,8 @@ static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
     return hipErrorInvalidValue;
   const int sm = make_layout(a.n).bytes();
   const long tasks = a.count * (1 + a.mhit);
-  if (hipMemsetAsync(a.mcnt, 0, sizeof(unsigned) * kMhrsCounters, st) != hipSuccess) return hipErrorUnknown;
+  /* (the queue counters are zeroed by round 0's block 0, every task's record
+   * is written by round 0: no fills per sweep) */
   {
     const int smc = sm + 16; /* + the claim cursor */
     /* persistent grid: exactly the resident blocks (a block that started
@@ -1190,7 +1198,6 @@ static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
     if (hipError_t e = launch_config(cfg, (const void *)mhrs_search<NT, 1, kMhrsK0>, smc, &occc, &cus);
         e != hipSuccess)
       return e;
-    if (hipMemsetAsync(a.mbest, 0xff, sizeof(uint32_t) * tasks, st) != hipSuccess) return hipErrorUnknown;
     /* compaction grids: after round 0 every task is scanned (~4096 per
      * block); the later queues are short */
     const dim3 g((unsigned)(cus * occc)), gc(256),
