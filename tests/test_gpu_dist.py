@@ -3,8 +3,8 @@
 The driver's scaling runs launch bench.py under torchrun with N > 1 ranks;
 the multi-rank arithmetic of phasetype_amd/dist.py is covered over gloo in
 test_multirank.py.  Here torchrun starts ONE rank on the GPU, which (WORLD_SIZE
-set) initialises the "nccl" (RCCL) process group and goes through the same
-code as N > 1: the statistics all-reduce every sweep (RCCL on the sweep
+set) initialises the "nccl" (RCCL) process group and, with
+PHT_WORLD1_REDUCE=1, goes through the same code as N > 1: the statistics all-reduce every sweep (RCCL on the sweep
 stream inside the library, Sweeper.attach_rccl), max-over-ranks timing, the
 weak-scaling side measurement.  It runs in a child process because
 torch must initialise the device before the library loads (bench.py's order;
@@ -29,12 +29,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_bench_under_torchrun_rccl(gpu):
+@pytest.mark.parametrize("reduce_at_world1", [True, False])
+def test_bench_under_torchrun_rccl(gpu, reduce_at_world1):
+    """With PHT_WORLD1_REDUCE=1 the one rank runs the N > 1 statistics path
+    (RCCL all-reduce on the sweep stream, self-tested at attach); by default
+    a world of one runs no collective (bench.py use_coll)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(REPO, "bench.py"), "--gpus", "1", "--steps", "4", "--warmup", "1",
            "--N", "200000", "--no-cpu-baseline"]
-    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
+    env = dict(os.environ, PHT_WORLD1_REDUCE="1" if reduce_at_world1 else "0")
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
@@ -42,7 +47,8 @@ def test_bench_under_torchrun_rccl(gpu):
     assert line["n_gpus"] == 1 and line["steps"] == 4
     assert line["value"] > 0 and line["ms_per_step"] > 0
     assert line["weak_scaling"]["N_total"] == 200000
-    assert line["config"]["stats_reduce"] == "rccl-in-stream (self-tested)"
+    want = "rccl-in-stream (self-tested)" if reduce_at_world1 else "none (world 1)"
+    assert line["config"]["stats_reduce"] == want
 
 
 def _chain_child(nproc):
