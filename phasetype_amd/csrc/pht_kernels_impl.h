@@ -244,24 +244,41 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
    * (extra words 8, 9, 10) and rounds 0 / 1 (11, 12 / 13, 14) */
   unsigned long long d_wit = 0, d_lit = 0, d_tail = 0;
 #endif
+#ifdef PHT_MHRS_STAMPS
+  /* diagnostic builds: wave cycles in the refill code (claim, item loads,
+   * stream init) and in the rest of the iteration, wave iterations, and the
+   * refill cycles and count of iterations in which a lane claimed an item
+   * (extra words 8..12; 13, 14: refill and all cycles of round 0) */
+  unsigned long long s_ref = 0, s_rest = 0, s_it = 0, s_cref = 0, s_cit = 0;
+  unsigned long long s_last = __builtin_amdgcn_s_memtime();
+  bool s_claimed = false;
+#endif
   for (;;) {
+#ifdef PHT_MHRS_STAMPS
+    s_claimed = false;
+#endif
     while (!inatt) { /* next attempt of this item, or the next item */
       if (!have) {
         if (item >= total) break;
         item = claim_pos(__hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), blk, nblk);
         if (item >= total) break;
+#ifdef PHT_MHRS_STAMPS
+        s_claimed = true;
+#endif
         const long q = item / W;
         l = (int)(item % W);
         task = qin ? qin[q] : (uint32_t)q;
         const long pos = task / T1;
         c = (int)(task % T1);
+        /* the item's three loads issued together (one memory latency per
+         * claim, not two) */
         cens = a.cens[pos];
+        y = a.y[pos];
+        gid = a.gid[pos];
         if (c > 0 && cens) { /* censored observations have no proposals */
           if (l == 0) a.mbest[task] = 0u;
           continue;
         }
-        y = a.y[pos];
-        gid = a.gid[pos];
         k = 0;
         have = true;
         lrec = 0xffffffffu;
@@ -295,6 +312,18 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
       inatt = true;
     }
     if (!__any(inatt)) break;
+#ifdef PHT_MHRS_STAMPS
+    unsigned long long s_t1;
+    {
+      /* (y, gid, cens of a claimed item are consumed in the refill code or
+       * by the stream's first block: make the stamp wait for them) */
+      __builtin_amdgcn_s_waitcnt(0);
+      s_t1 = __builtin_amdgcn_s_memtime();
+      s_ref += s_t1 - s_last;
+      s_it++;
+      if (__any(s_claimed)) { s_cref += s_t1 - s_last; s_cit++; }
+    }
+#endif
 #ifdef PHT_MHRS_DIAG
     {
       const unsigned act = (unsigned)__popcll(__ballot(inatt));
@@ -373,7 +402,26 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
         }
       }
     }
+#ifdef PHT_MHRS_STAMPS
+    {
+      __builtin_amdgcn_s_waitcnt(0);
+      const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+      s_rest += t2 - s_t1;
+      s_last = t2;
+    }
+#endif
   }
+#ifdef PHT_MHRS_STAMPS
+  if ((threadIdx.x & 63u) == 0u) {
+    unsigned long long *x = a.stats + 2 * a.n + a.n * a.n;
+    atomicAdd(&x[8], s_ref);
+    atomicAdd(&x[9], s_rest);
+    atomicAdd(&x[10], s_it);
+    atomicAdd(&x[11], s_cref);
+    atomicAdd(&x[12], s_cit);
+    if (A0 == 0u) { atomicAdd(&x[13], s_ref); atomicAdd(&x[14], s_ref + s_rest); }
+  }
+#endif
 #ifdef PHT_MHRS_DIAG
   if ((threadIdx.x & 63u) == 0u) {
     unsigned long long *x = a.stats + 2 * a.n + a.n * a.n;
