@@ -65,6 +65,8 @@ int pht_ctx_sweep(pht_ctx *c, const double *S, const double *s, uint32_t k0, uin
 int pht_ctx_sweep_debug(pht_ctx *c, const double *S, const double *s, uint32_t k0, uint32_t k1, uint32_t sweep,
                         int zexp, long long *stats_out, int *B, int *pre, int *flags, uint32_t *ndraw,
                         long long *zq, int *N);
+/* Device time of the last sweep's kernels (HIP events); -1 when that sweep
+ * was not timed (pht_gibbs_run times one sweep in PHT_KTIME_EVERY). */
 float pht_ctx_last_kernel_ms(pht_ctx *c);
 /* Observation-sweeps flagged in the last pht_gibbs_run / pht_gibbs_run_chains
  * on this context (node-wide, after the reduce): a cap (ARMS iterations, path
@@ -85,7 +87,10 @@ int pht_ctx_set_global_count(pht_ctx *c, long long total);
  * an RCCL communicator attached: passing both is an error, the block would be
  * summed twice).  Every sweep is checked: the node-wide processed count must
  * equal the observations (see pht_ctx_set_global_count), and the fixed-point
- * z sums must not overflow int64; either failure ends the run with an error. */
+ * z sums must not overflow int64; either failure ends the run with an error.
+ * kernel_ms_total: the sweeps' device time, measured by HIP events on one
+ * sweep in PHT_KTIME_EVERY (default 4; the events cost the GPU ~9 us of idle
+ * time per timed sweep) and scaled to all it - 1 sweeps from their mean. */
 typedef int (*pht_reduce_fn)(long long *stats, int len, void *user);
 int pht_gibbs_run(pht_ctx *c, int it, int method, int m, const double *nu, const double *zeta, const int *T,
                   const double *C, int zexp, int silent, const double *start, double *res, pht_reduce_fn reduce,

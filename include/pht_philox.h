@@ -41,7 +41,24 @@ PHT_HD2 uint32_t pht_mulhilo(uint32_t a, uint32_t b, uint32_t *hi) {
   return (uint32_t)p;
 }
 
+PHT_HD2 pht_u32x4 pht_philox_round(pht_u32x4 c, uint32_t k0, uint32_t k1) {
+  uint32_t hi0, hi1;
+  const uint32_t lo0 = pht_mulhilo(0xD2511F53U, c.v[0], &hi0);
+  const uint32_t lo1 = pht_mulhilo(0xCD9E8D57U, c.v[2], &hi1);
+  pht_u32x4 o;
+  o.v[0] = hi1 ^ c.v[1] ^ k0;
+  o.v[1] = lo1;
+  o.v[2] = hi0 ^ c.v[3] ^ k1;
+  o.v[3] = lo0;
+  return o;
+}
+
+/* (device: the compiler keeps the ten rounds as a loop of two; compilation
+ * units built with PHT_PHILOX_UNROLL unroll them, see phasetype_amd/build.py) */
 PHT_HD2 pht_u32x4 pht_philox4x32_10(pht_u32x4 c, uint32_t k0, uint32_t k1) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PHT_PHILOX_UNROLL)
+#pragma unroll
+#endif
   for (int r = 0; r < 10; r++) {
     uint32_t hi0, hi1;
     uint32_t lo0 = pht_mulhilo(0xD2511F53U, c.v[0], &hi0);
@@ -129,6 +146,31 @@ PHT_HD2 void pht_stream_topup(pht_stream *s) {
     s->nb = 1;
   }
 }
+
+#if defined(__HIPCC__)
+/* pht_stream_topup with the block's ten rounds unrolled (the same words):
+ * for a kernel whose unit keeps the loop elsewhere (the MHRS search at
+ * n = 15, PHT_MHRS_PHILOX_UNROLL) */
+__device__ __forceinline__ void pht_stream_topup_unrolled(pht_stream *s) {
+  if (!s->nb) {
+    pht_u32x4 c;
+    c.v[0] = s->obs; c.v[1] = s->tag; c.v[2] = s->sweep; c.v[3] = s->blk++;
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t k0 = __builtin_amdgcn_readfirstlane(s->k0), k1 = __builtin_amdgcn_readfirstlane(s->k1);
+#else
+    uint32_t k0 = s->k0, k1 = s->k1;
+#endif
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+      c = pht_philox_round(c, k0, k1);
+      k0 += 0x9E3779B9U;
+      k1 += 0xBB67AE85U;
+    }
+    s->b0 = c.v[0]; s->b1 = c.v[1]; s->b2 = c.v[2]; s->b3 = c.v[3];
+    s->nb = 1;
+  }
+}
+#endif
 
 PHT_HD2 uint32_t pht_next_w(pht_stream *s) {
   if (s->na == 0) {

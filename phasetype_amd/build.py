@@ -26,8 +26,15 @@ KERNEL_NTS = (10, 3, 5, 15, 20, 0)  # compile-time n of the kernels (0 = runtime
 # interleaved A/Bs on two boxes (profiles/r05/sched_flags/); not for n = 15,
 # where cfg5 ECS lost 0.9 / 2.4 %
 UNIT_FLAGS = {10: ("-mllvm", "--amdgpu-schedule-metric-bias=0")}
+# Philox blocks with their ten rounds unrolled (the compiler keeps a loop of
+# two rounds otherwise; the same words): every kernel of the n = 5 and n = 20
+# units (cfg2 -4.1 %, cfg3 -1.4 % per sweep) and the MHRS search of the
+# n = 15 unit (cfg5 MHRS -1.4 %; the n = 15 ECS kernels lost 3.9 % with it);
+# neutral at n = 3 and n = 10, which keep the loop (profiles/r06/unroll/)
+UNIT_DEFINES = {5: ("PHT_PHILOX_UNROLL",), 20: ("PHT_PHILOX_UNROLL",), 15: ("PHT_MHRS_PHILOX_UNROLL",)}
 # (source, extra defines, extra device-compile flags) per object
-UNITS = [("pht_kernels_nt.hip", (f"PHT_NT={k}",), UNIT_FLAGS.get(k, ())) for k in KERNEL_NTS] + [
+UNITS = [("pht_kernels_nt.hip", (f"PHT_NT={k}",) + UNIT_DEFINES.get(k, ()), UNIT_FLAGS.get(k, ()))
+         for k in KERNEL_NTS] + [
     ("pht_dispatch.hip", (), ()), ("pht_resident.hip", (), ()), ("gibbs_host.cpp", (), ()), ("rstream.c", (), ())]
 SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = ["pht_device.h", "pht_env.h", "pht_kernels.h", "pht_kernels_impl.h", "pht_layout.h", "rstream.h",

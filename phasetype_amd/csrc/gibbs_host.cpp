@@ -475,6 +475,9 @@ struct pht_ctx {
   long dbg_cap = 0;
   float last_ms = 0.f;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  /* this sweep records ev0 / ev1 around its kernels (ctx_enqueue): the Gibbs
+   * loop times one sweep in PHT_KTIME_EVERY (gibbs_run), single sweeps always */
+  bool ktimed = true;
   /* ECS: the censored range runs on stream2, concurrently with the exact range */
   hipStream_t stream2 = nullptr;
   hipEvent_t evf = nullptr, evj = nullptr;
@@ -1210,8 +1213,10 @@ static int ctx_launch(pht_ctx *c, const SweepArgs &a, bool debug) {
   return 0;
 }
 
-static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int zexp, bool debug) {
+static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int zexp, bool debug,
+                       bool timed = true) {
   HIPCHK(hipSetDevice(c->device));
+  c->ktimed = timed;
   const int pb = make_layout(c->n).bytes();
   const int sl = stats_len(c->n);
   HIPCHK(hipMemcpyAsync(c->d_params, c->h_params, pb, hipMemcpyHostToDevice, c->stream));
@@ -1265,9 +1270,12 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     a.dbg_ndraw = c->d_ndraw;
   }
   if (c->method == kMethodUNIF && unif_prepare(c, a)) return -1;
-  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  /* the kernel-time markers: the GPU idles while the host enqueues them
+   * (~9 us per sweep at cfg4, profiles/r06/kernel_events/), so the Gibbs loop
+   * records them on a sample of its sweeps only */
+  if (timed) HIPCHK(hipEventRecord(c->ev0, c->stream));
   if (ctx_launch(c, a, debug)) return -1;
-  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  if (timed) HIPCHK(hipEventRecord(c->ev1, c->stream));
   if (c->comm) {
     /* multi-process: the block summed over all ranks in place, on the sweep's
      * stream, before the one copy to the host (pht_ctx_attach_rccl) */
@@ -1335,17 +1343,20 @@ static int ctx_wait(pht_ctx *c) {
   if (c->h_out) {
     if (wait_stats_flag(c)) return -1;
     memcpy(c->h_stats, c->h_out, sizeof(unsigned long long) * stats_len(c->n));
-    /* ev1 precedes the publishing kernel on the stream: it has completed */
-    hipError_t e = hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
-    if (e == hipErrorNotReady) {
-      HIPCHK(hipEventSynchronize(c->ev1));
-      e = hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+    if (c->ktimed) {
+      /* ev1 precedes the publishing kernel on the stream: it has completed */
+      hipError_t e = hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+      if (e == hipErrorNotReady) {
+        HIPCHK(hipEventSynchronize(c->ev1));
+        e = hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+      }
+      HIPCHK(e);
     }
-    HIPCHK(e);
   } else {
     HIPCHK(hipEventSynchronize(c->evd));
-    HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    if (c->ktimed) HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
   }
+  if (!c->ktimed) c->last_ms = -1.f; /* not measured this sweep */
   if (c->method == kMethodMHRS && c->d_mcnt && getenv("PHT_MHRS_COUNTS")) {
     /* diagnostics: tasks still unresolved after MHRS search rounds 0..4 */
     unsigned q[5];
@@ -1530,7 +1541,14 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
   std::vector<unsigned char> pb;
   say("Starting phase-type MCMC sampler ...\n\nBegining processing ...");
   if (silent) say(" silent processing selected, there will be no further feedback until MCMC run complete");
+  /* kernel time: the sweeps' events on one sweep in `every` (the last of
+   * each group, so a fresh chain's first and slowest sweeps do not weigh
+   * more than their share; PHT_KTIME_EVERY, default 4, 1 = every sweep; the
+   * last sweep when no other was timed), the total scaled from their mean;
+   * chain groups time every sweep */
+  const int every = std::max(1, getenv("PHT_KTIME_EVERY") ? atoi(getenv("PHT_KTIME_EVERY")) : 4);
   double kms = 0.0;
+  long ktimed = 0;
   long long flagged = 0;
   int first_flagged = 0;
   /* every sweep must account for every observation of every shard: the
@@ -1566,19 +1584,25 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
     const int bm = ctxs[0]->ulaw ? kMethodUNIF : (disp == kMethodMHRS ? kMethodMHRS : method);
     const int info = build_params(n, G.S.data(), G.s.data(), bm, pb);
     if (info < 0) return -1;
+    const bool timed = iter % every == 0 || (iter == it - 1 && ktimed == 0);
     for (pht_ctx *c : ctxs) {
       memcpy(c->h_params, pb.data(), pb.size());
       if (c->grp) {
         if (group_sweep(c, k0, k1, (uint32_t)iter, zexp)) return -1;
-      } else if (ctx_enqueue(c, k0, k1, (uint32_t)iter, zexp, false)) {
+      } else if (ctx_enqueue(c, k0, k1, (uint32_t)iter, zexp, false, timed)) {
         return -1;
       }
     }
     std::fill(tot.begin(), tot.end(), 0LL);
     bool wrapped = false;
+    bool any_t = false;
+    double ksum = 0.0;
     for (pht_ctx *c : ctxs) {
       if (!c->grp && ctx_wait(c)) return -1;
-      kms += c->last_ms;
+      if (c->last_ms >= 0.f) {
+        ksum += c->last_ms;
+        any_t = true;
+      }
       for (int k = 0; k < sl; k++) wrapped |= __builtin_add_overflow(tot[k], (long long)c->h_stats[k], &tot[k]);
     }
     if (reduce && reduce(tot.data(), sl, reduce_user) != 0) {
@@ -1618,9 +1642,14 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
       return -1;
     }
 #endif
+    if (any_t) {
+      kms += ksum;
+      ktimed++;
+    }
     for (int k = 0; k < n; k++) z[k] = ldexp((double)tot[k], -zexp);
     G.update(R, iter, z.data(), tot.data() + 2 * n);
   }
+  if (ktimed > 0) kms = kms / (double)ktimed * (double)(it - 1);
   for (pht_ctx *c : ctxs) c->flagged = flagged;
   if (flagged)
     warn("\nWARNING: %lld observation-sweeps hit a sampler cap or numerical guard (first in iteration %d); "

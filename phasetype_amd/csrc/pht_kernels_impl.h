@@ -178,6 +178,12 @@ constexpr MhrsRound kMhrsRounds[5] = {
     {4, 32, 16}, {32, 32, 144}, {512, 32, 1168}, {8192, 32, 17552}, {131072, 32, 279696}};
 #endif
 
+/* the MHRS search's per-row running sums of Pfull over the successor list
+ * (mhrs_search_body), after the parameter block and the claim cursor; only
+ * where they cost no occupancy (n <= 15: at n = 20 the block's LDS would
+ * drop the search from 4 to 3 blocks per CU) */
+__host__ __device__ inline int mhrs_cum_bytes(int n) { return n <= 15 ? n * (n + 1) * 8 : 0; }
+
 template <int NT>
 __device__ __forceinline__ Par<NT> stage_params(const SweepArgs &a, PHT_LDS unsigned char *lsm) {
   const int n = nval<NT>(a.n);
@@ -225,6 +231,44 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
   pht_stage_math_tables();
   __syncthreads();
   const int n = P.n();
+  /* the jump's categorical scan adds Pfull[j, k] over j's successor list in
+   * order and stops at the first running sum >= its uniform: the running
+   * sums, the same additions in the same order, are formed once per block
+   * (row j: cum[j (n + 1) + q]), so the scan reads a sum and a successor
+   * with no dependent load and no addition (the same state every time) */
+  /* (round 0 only: in the later rounds the sums' loads cost 4 VGPRs, 7 -> 6
+   * waves per SIMD at n = 10, and the round ran slower, cfg4 MHRS +3.4 %
+   * against -3.0 % with round 0 alone; profiles/r06/mhrs_cum/) */
+#ifdef PHT_MHRS_CUM_ALL
+  const bool usecum = mhrs_cum_bytes(n) > 0;
+#else
+  const bool usecum = mhrs_cum_bytes(n) > 0 && W == 1;
+#endif
+  PHT_LDS double *cum = (PHT_LDS double *)((PHT_LDS unsigned char *)cursor + 16);
+  if (usecum) {
+    if ((int)threadIdx.x < n) {
+      const int jr = threadIdx.x, cnt = P.nsuccPf(jr);
+      double sofar = 0.0;
+      for (int q = 0; q < cnt; q++) {
+        sofar += P.Pf(jr, P.succPf(jr, q));
+        cum[jr * (n + 1) + q] = sofar;
+      }
+    }
+    __syncthreads();
+  }
+  /* the start-state scan's result when it does not depend on the draw: pi's
+   * first nonzero entry is >= 1 (pi = e_1 in every LJMA_Gibbs sweep,
+   * src/PHT_MCMC_Aslett.c:190-193): the scan stops there for every uniform
+   * in (0, 1), so an attempt takes that state (its uniform still drawn) */
+  int pifix = -1;
+  for (int i = 0; i < n; i++) {
+    const double pv = P.pi(i);
+    if (!(pv == 0.0)) {
+      pifix = (pv >= 1.0) ? i : -1;
+      break;
+    }
+  }
+  pifix = __builtin_amdgcn_readfirstlane(pifix); /* (the same in every lane: a scalar) */
   long item = 0;
   /* item state */
   bool have = false;
@@ -337,7 +381,11 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
      * lanes whose buffer ran dry would, one draw site at a time); a step
      * uses at most 4 words (start draw + a jump's 3), and the buffer then
      * holds >= 4 (same word sequence either way) */
+#ifdef PHT_MHRS_PHILOX_UNROLL
+    if (inatt) pht_stream_topup_unrolled(&r);
+#else
     if (inatt) pht_stream_topup(&r);
+#endif
     /* several lanes per task (rounds 1-5): an attempt above the task's
      * record can no longer be the first success; the record is read here and
      * tested after the jump (the load's latency hidden by the jump), and such
@@ -351,9 +399,12 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
     }
     if (inatt && fresh) { /* start state of the attempt */
       const double target = pht_next_u(&r);
-      double sofar = 0.0;
-      int B2 = 0;
-      while (sofar < target && B2 <= n) sofar += (B2 < n ? P.pi(B2) : 0.0), B2++;
+      int B2 = pifix + 1;
+      if (pifix < 0) {
+        double sofar = 0.0;
+        B2 = 0;
+        while (sofar < target && B2 <= n) sofar += (B2 < n ? P.pi(B2) : 0.0), B2++;
+      }
       j = lastj = B2 - 1;
       t = 0.0;
       nj = 0;
@@ -369,14 +420,25 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
           t = t + dev_rexp(r, P.scale(j)) /* = 1.0 / -S_jj, per sweep (pht_layout.h) */;
           const double target = pht_next_u(&r);
           const int cnt = P.nsuccPf(j);
-          double sofar = 0.0;
           int sel = n + 1;
-          for (int q = 0; q < cnt; q++) {
-            const int kk = P.succPf(j, q);
-            sofar += P.Pf(j, kk);
-            if (!(sofar < target)) {
-              sel = kk;
-              break;
+          if (usecum) {
+            for (int q = 0; q < cnt; q++) {
+              const double cq = cum[j * (n + 1) + q];
+              const int kk = P.succPf(j, q);
+              if (!(cq < target)) {
+                sel = kk;
+                break;
+              }
+            }
+          } else {
+            double sofar = 0.0;
+            for (int q = 0; q < cnt; q++) {
+              const int kk = P.succPf(j, q);
+              sofar += P.Pf(j, kk);
+              if (!(sofar < target)) {
+                sel = kk;
+                break;
+              }
             }
           }
           j = sel;
@@ -434,9 +496,14 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
 #endif
 }
 
+#ifdef PHT_MHRS_W7
+#define PHT_MHRS_WAVES __attribute__((amdgpu_waves_per_eu(7)))
+#else
+#define PHT_MHRS_WAVES
+#endif
 template <int NT, int W, int K>
-__global__ void __launch_bounds__(kBlock) mhrs_search(SweepArgs a, uint32_t A0, const uint32_t *qin,
-                                                      const unsigned *cin) {
+__global__ void __launch_bounds__(kBlock) PHT_MHRS_WAVES mhrs_search(SweepArgs a, uint32_t A0, const uint32_t *qin,
+                                                                     const unsigned *cin) {
   mhrs_search_body<NT, W, K>(a, A0, qin, cin, blockIdx.x, gridDim.x);
 }
 
@@ -1237,7 +1304,7 @@ static hipError_t launch_mhrs_search(const SweepArgs &a, hipStream_t st) {
   /* (the queue counters are zeroed by round 0's block 0, every task's record
    * is written by round 0: no fills per sweep) */
   {
-    const int smc = sm + 16; /* + the claim cursor */
+    const int smc = sm + 16 + mhrs_cum_bytes(a.n); /* + the claim cursor, the running sums */
     /* persistent grid: exactly the resident blocks (a block that started
      * late would still own its share of the claim chunks); the rounds'
      * instantiations share one resource footprint */
@@ -1707,7 +1774,7 @@ static hipError_t launch_chains(const SweepArgs *h, const SweepArgs *d, int K, i
       maxt = std::max(maxt, h[c].count * (1 + h[c].mhit));
     }
     if (maxc < 1) return hipSuccess;
-    const int smc = make_layout(h[0].n).bytes() + 16;
+    const int smc = make_layout(h[0].n).bytes() + 16 + mhrs_cum_bytes(h[0].n);
     static LaunchCfg cfg;
     int occ = 0, cus = 0;
     if (hipError_t e = launch_config(cfg, (const void *)mhrs_search_chains<NT, 1, kMhrsK0>, smc, &occ, &cus);

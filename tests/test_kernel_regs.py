@@ -39,13 +39,14 @@ def test_ecs_two_waves_no_spill(regs, nt, kind):
 
 
 @pytest.mark.parametrize("kind,ceiling", [("ecs_exact_kernelILi20ELb0ELb0EE", 43),
-                                          ("ecs_exact_kernelILi20ELb0ELb1EE", 130),
+                                          ("ecs_exact_kernelILi20ELb0ELb1EE", 145),
                                           ("ecs_chains_kernelILi20EE", 43)])
 def test_ecs_n20_spill_ceiling(regs, kind, ceiling):
     """n = 20 runs two waves per SIMD with some VGPRs spilled (faster than one
     wave without spills: cfg3 kernel 0.812 vs 0.865 ms, profiles/r05/cfg3/
     w1_ab_*.jsonl); the r04 counts are the ceiling, so the spills cannot grow
-    unnoticed."""
+    unnoticed.  (The row kernel's 130 -> 145 in r06: its unit's Philox rounds
+    unrolled, 142 spilled, cfg3 -1.4 % per sweep, profiles/r06/unroll/.)"""
     hits = {k: v for k, v in regs.items() if kind in k}
     assert len(hits) == 1, (kind, list(hits))
     (name, d), = hits.items()
