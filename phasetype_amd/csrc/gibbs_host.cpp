@@ -475,9 +475,6 @@ struct pht_ctx {
   long dbg_cap = 0;
   float last_ms = 0.f;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  /* this sweep records ev0 / ev1 around its kernels (ctx_enqueue): the Gibbs
-   * loop times one sweep in PHT_KTIME_EVERY (gibbs_run), single sweeps always */
-  bool ktimed = true;
   /* ECS: the censored range runs on stream2, concurrently with the exact range */
   hipStream_t stream2 = nullptr;
   hipEvent_t evf = nullptr, evj = nullptr;
@@ -496,6 +493,23 @@ struct pht_ctx {
   unsigned long long *h_out = nullptr, *d_out = nullptr;
   unsigned *h_flag = nullptr, *d_flag = nullptr;
   unsigned seq = 0;
+  /* sweeps enqueued and not yet waited for (oldest first): the statistics
+   * flag value each publishes and its kernel-time event pair; two in flight
+   * in the pipelined Gibbs loop (gibbs_run), else one */
+  struct Inflight {
+    unsigned seq = 0, gate = 0;
+    bool timed = false;
+    int evs = 0;
+  } infl[2];
+  int nin = 0;
+  unsigned nenq = 0;
+  hipEvent_t ev0b = nullptr, ev1b = nullptr;
+  /* the pipelined loop's gate (pht_gate_kernel): word 0 the released value
+   * (host writes), word 16 the device's ack; the parameter block staged in
+   * coherent pinned memory for the gate kernel's copy */
+  unsigned *h_gate = nullptr, *d_gate = nullptr;
+  unsigned long long *h_pg = nullptr, *d_pg = nullptr;
+  unsigned gate_seq = 0;
 };
 
 /* lanes of the persistent ECS grid on an MI355X (256 CUs x 2 blocks x 256) */
@@ -970,6 +984,26 @@ extern "C" pht_ctx *pht_ctx_create(int device, int n, int method, int mhit) {
       (void)hipGetLastError();
     }
   }
+  /* the pipelined loop's gate and staged parameters (optional: without them,
+   * or with PHT_PIPELINE=0, the loop enqueues each sweep after the last) */
+  if (c->h_out && !(getenv("PHT_PIPELINE") && !strcmp(getenv("PHT_PIPELINE"), "0"))) {
+    void *hg = nullptr, *hp = nullptr, *dg = nullptr, *dp = nullptr;
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+    if (hipEventCreate(&c->ev0b) == hipSuccess && hipEventCreate(&c->ev1b) == hipSuccess &&
+        hipHostMalloc(&hg, 128, fl) == hipSuccess && hipHostMalloc(&hp, make_layout(n).bytes(), fl) == hipSuccess &&
+        hipHostGetDevicePointer(&dg, hg, 0) == hipSuccess && hipHostGetDevicePointer(&dp, hp, 0) == hipSuccess) {
+      c->h_gate = static_cast<unsigned *>(hg);
+      c->d_gate = static_cast<unsigned *>(dg);
+      c->h_pg = static_cast<unsigned long long *>(hp);
+      c->d_pg = static_cast<unsigned long long *>(dp);
+      c->h_gate[0] = 0u;
+      c->h_gate[16] = 0u;
+    } else {
+      if (hg) (void)hipHostFree(hg);
+      if (hp) (void)hipHostFree(hp);
+      (void)hipGetLastError();
+    }
+  }
   return c;
 }
 
@@ -989,6 +1023,10 @@ extern "C" void pht_ctx_destroy(pht_ctx *c) {
   if (c->evd) (void)hipEventDestroy(c->evd);
   if (c->h_out) (void)hipHostFree(c->h_out);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
+  if (c->h_gate) (void)hipHostFree(c->h_gate);
+  if (c->h_pg) (void)hipHostFree(c->h_pg);
+  if (c->ev0b) (void)hipEventDestroy(c->ev0b);
+  if (c->ev1b) (void)hipEventDestroy(c->ev1b);
   if (c->comm) rccl_destroy(c->comm);
   if (c->d_rccl) (void)hipFree(c->d_rccl);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
@@ -1213,13 +1251,26 @@ static int ctx_launch(pht_ctx *c, const SweepArgs &a, bool debug) {
   return 0;
 }
 
+/* gate != 0: the pipelined loop's next sweep, enqueued while the current one
+ * runs; its parameters come from c->h_pg once the host releases `gate`
+ * (pht_gate_kernel), not from c->h_params now */
 static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int zexp, bool debug,
-                       bool timed = true) {
+                       bool timed = true, unsigned gate = 0) {
   HIPCHK(hipSetDevice(c->device));
-  c->ktimed = timed;
+  if (c->nin >= 2 || (gate && (c->nin != 1 || !c->h_gate || !c->h_out))) {
+    set_err("internal: sweep enqueued with %d in flight (gate %u)", c->nin, gate);
+    return -1;
+  }
   const int pb = make_layout(c->n).bytes();
   const int sl = stats_len(c->n);
-  HIPCHK(hipMemcpyAsync(c->d_params, c->h_params, pb, hipMemcpyHostToDevice, c->stream));
+  const int evs = (int)(c->nenq++ & 1u) && c->ev0b ? 1 : 0;
+  hipEvent_t e0 = evs ? c->ev0b : c->ev0, e1 = evs ? c->ev1b : c->ev1;
+  if (gate) {
+    HIPCHK(pht_launch_gate(c->d_gate, gate, c->d_pg, reinterpret_cast<unsigned long long *>(c->d_params), pb / 8,
+                           c->d_gate + 16, c->stream));
+  } else {
+    HIPCHK(hipMemcpyAsync(c->d_params, c->h_params, pb, hipMemcpyHostToDevice, c->stream));
+  }
   /* the block is zeroed at the end of the previous sweep, after its copy to
    * the host (off the critical path: it runs while the host does the Gamma
    * update); only the first sweep, or one after a failed enqueue, zeroes it
@@ -1273,9 +1324,9 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   /* the kernel-time markers: the GPU idles while the host enqueues them
    * (~9 us per sweep at cfg4, profiles/r06/kernel_events/), so the Gibbs loop
    * records them on a sample of its sweeps only */
-  if (timed) HIPCHK(hipEventRecord(c->ev0, c->stream));
+  if (timed) HIPCHK(hipEventRecord(e0, c->stream));
   if (ctx_launch(c, a, debug)) return -1;
-  if (timed) HIPCHK(hipEventRecord(c->ev1, c->stream));
+  if (timed) HIPCHK(hipEventRecord(e1, c->stream));
   if (c->comm) {
     /* multi-process: the block summed over all ranks in place, on the sweep's
      * stream, before the one copy to the host (pht_ctx_attach_rccl) */
@@ -1298,7 +1349,20 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
     HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * sl, c->stream));
   }
   c->stats_zero = true;
+  pht_ctx::Inflight &f = c->infl[c->nin++];
+  f.seq = c->seq;
+  f.gate = gate;
+  f.timed = timed;
+  f.evs = evs;
   return 0;
+}
+
+/* release the pipelined sweep waiting at `gate`: its parameter block (pb
+ * bytes) into the staging buffer, then the gate word (release store; the
+ * gate kernel's acquire load orders its copy after it) */
+static void ctx_release(pht_ctx *c, unsigned gate, const unsigned char *pb, size_t bytes) {
+  if (pb) memcpy(c->h_pg, pb, bytes);
+  __atomic_store_n(c->h_gate, gate, __ATOMIC_RELEASE);
 }
 
 /* the flag pht_stats_out_kernel sets for this sweep; the stream is queried
@@ -1308,22 +1372,22 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
  * its core to the others' host work instead of pausing on it */
 static std::atomic<int> g_stat_waiters{0};
 
-static int wait_stats_flag_spin(pht_ctx *c);
-static int wait_stats_flag(pht_ctx *c) {
+static int wait_stats_flag_spin(pht_ctx *c, unsigned want);
+static int wait_stats_flag(pht_ctx *c, unsigned want) {
   g_stat_waiters.fetch_add(1, std::memory_order_relaxed);
-  const int rc = wait_stats_flag_spin(c);
+  const int rc = wait_stats_flag_spin(c, want);
   g_stat_waiters.fetch_sub(1, std::memory_order_relaxed);
   return rc;
 }
 
-static int wait_stats_flag_spin(pht_ctx *c) {
+static int wait_stats_flag_spin(pht_ctx *c, unsigned want) {
   for (unsigned long spin = 1;; spin++) {
-    if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == c->seq) return 0;
+    if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == want) return 0;
     if (g_stat_waiters.load(std::memory_order_relaxed) > 1) sched_yield();
     if ((spin & 1023ul) == 0ul) {
       const hipError_t e = hipStreamQuery(c->stream);
       if (e == hipSuccess) {
-        if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == c->seq) return 0;
+        if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == want) return 0;
         set_err("device %d: the sweep finished without publishing its statistics", c->device);
         return -1;
       }
@@ -1338,25 +1402,40 @@ static int wait_stats_flag_spin(pht_ctx *c) {
   }
 }
 
+/* the oldest sweep in flight: its statistics into c->h_stats, its kernel
+ * time into c->last_ms (-1 when it was not timed) */
 static int ctx_wait(pht_ctx *c) {
   HIPCHK(hipSetDevice(c->device));
+  if (c->nin < 1) {
+    set_err("internal: no sweep in flight");
+    return -1;
+  }
+  const pht_ctx::Inflight f = c->infl[0];
+  c->infl[0] = c->infl[1];
+  c->nin--;
+  hipEvent_t e0 = f.evs ? c->ev0b : c->ev0, e1 = f.evs ? c->ev1b : c->ev1;
   if (c->h_out) {
-    if (wait_stats_flag(c)) return -1;
+    if (wait_stats_flag(c, f.seq)) return -1;
     memcpy(c->h_stats, c->h_out, sizeof(unsigned long long) * stats_len(c->n));
-    if (c->ktimed) {
+    if (f.gate && __atomic_load_n(c->h_gate + 16, __ATOMIC_ACQUIRE) != f.gate) {
+      set_err("device %d: a pipelined sweep's parameters were not released in time (gate %u, ack %u)", c->device,
+              f.gate, __atomic_load_n(c->h_gate + 16, __ATOMIC_ACQUIRE));
+      return -1;
+    }
+    if (f.timed) {
       /* ev1 precedes the publishing kernel on the stream: it has completed */
-      hipError_t e = hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+      hipError_t e = hipEventElapsedTime(&c->last_ms, e0, e1);
       if (e == hipErrorNotReady) {
-        HIPCHK(hipEventSynchronize(c->ev1));
-        e = hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+        HIPCHK(hipEventSynchronize(e1));
+        e = hipEventElapsedTime(&c->last_ms, e0, e1);
       }
       HIPCHK(e);
     }
   } else {
     HIPCHK(hipEventSynchronize(c->evd));
-    if (c->ktimed) HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    if (f.timed) HIPCHK(hipEventElapsedTime(&c->last_ms, e0, e1));
   }
-  if (!c->ktimed) c->last_ms = -1.f; /* not measured this sweep */
+  if (!f.timed) c->last_ms = -1.f; /* not measured this sweep */
   if (c->method == kMethodMHRS && c->d_mcnt && getenv("PHT_MHRS_COUNTS")) {
     /* diagnostics: tasks still unresolved after MHRS search rounds 0..4 */
     unsigned q[5];
@@ -1547,9 +1626,31 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
    * last sweep when no other was timed), the total scaled from their mean;
    * chain groups time every sweep */
   const int every = std::max(1, getenv("PHT_KTIME_EVERY") ? atoi(getenv("PHT_KTIME_EVERY")) : 4);
+  auto want_time = [&](int k) { return k % every == 0 || (k == it - 1 && k - 1 < every); };
   double kms = 0.0;
   long ktimed = 0;
   long long flagged = 0;
+  /* Pipelined loop (one context, not a chains group, not UNIF, whose enqueue
+   * reads the parameters): sweep k + 1 is enqueued as soon as sweep k is,
+   * behind a gate kernel that waits for its parameters, so the launch work
+   * runs while sweep k does and only the Gamma update and the next
+   * parameter block stay between two sweeps (PHT_PIPELINE=0: off).  The
+   * draws are the same: sweep k + 1's parameters are those the update
+   * produced from sweep k's statistics. */
+  pht_ctx *pc = ctxs.size() == 1 ? ctxs[0] : nullptr;
+  const bool pipe = pc && !pc->grp && pc->h_gate && pc->method != kMethodUNIF && !pc->ulaw && it > 2;
+  bool pending = false;
+  unsigned pgate = 0;
+  /* an early return with a gated sweep enqueued: release it (it runs on the
+   * last staged parameters) and drain the stream, so nothing waits on a gate */
+  auto unwind = [&]() {
+    if (pending) {
+      ctx_release(pc, pgate, nullptr, 0);
+      (void)hipStreamSynchronize(pc->stream);
+      pc->nin = 0;
+      pending = false;
+    }
+  };
   int first_flagged = 0;
   /* every sweep must account for every observation of every shard: the
    * node-wide processed count (extra word kXObs, after the reduce) is checked
@@ -1583,22 +1684,46 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
     /* bridge contexts run the UNIF kernels: their block needs no eigensystem */
     const int bm = ctxs[0]->ulaw ? kMethodUNIF : (disp == kMethodMHRS ? kMethodMHRS : method);
     const int info = build_params(n, G.S.data(), G.s.data(), bm, pb);
-    if (info < 0) return -1;
-    const bool timed = iter % every == 0 || (iter == it - 1 && ktimed == 0);
-    for (pht_ctx *c : ctxs) {
-      memcpy(c->h_params, pb.data(), pb.size());
-      if (c->grp) {
-        if (group_sweep(c, k0, k1, (uint32_t)iter, zexp)) return -1;
-      } else if (ctx_enqueue(c, k0, k1, (uint32_t)iter, zexp, false, timed)) {
+    if (info < 0) {
+      unwind();
+      return -1;
+    }
+    const bool timed = want_time(iter);
+    if (pending) {
+      memcpy(pc->h_params, pb.data(), pb.size());
+      ctx_release(pc, pgate, pb.data(), pb.size());
+      pending = false;
+    } else {
+      for (pht_ctx *c : ctxs) {
+        memcpy(c->h_params, pb.data(), pb.size());
+        if (c->grp) {
+          if (group_sweep(c, k0, k1, (uint32_t)iter, zexp)) return -1;
+        } else if (ctx_enqueue(c, k0, k1, (uint32_t)iter, zexp, false, timed)) {
+          return -1;
+        }
+      }
+    }
+    if (pipe && iter + 1 < it) {
+      if (++pc->gate_seq == 0u) pc->gate_seq = 1u;
+      pgate = pc->gate_seq;
+      if (ctx_enqueue(pc, k0, k1, (uint32_t)(iter + 1), zexp, false, want_time(iter + 1), pgate)) {
+        /* (a failed enqueue may have left the gate kernel in the stream) */
+        ctx_release(pc, pgate, nullptr, 0);
+        (void)hipStreamSynchronize(pc->stream);
+        pc->nin = 0;
         return -1;
       }
+      pending = true;
     }
     std::fill(tot.begin(), tot.end(), 0LL);
     bool wrapped = false;
     bool any_t = false;
     double ksum = 0.0;
     for (pht_ctx *c : ctxs) {
-      if (!c->grp && ctx_wait(c)) return -1;
+      if (!c->grp && ctx_wait(c)) {
+        unwind();
+        return -1;
+      }
       if (c->last_ms >= 0.f) {
         ksum += c->last_ms;
         any_t = true;
@@ -1607,6 +1732,7 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
     }
     if (reduce && reduce(tot.data(), sl, reduce_user) != 0) {
       set_err("statistics all-reduce callback failed at sweep %d", iter);
+      unwind();
       return -1;
     }
 #ifndef PHT_STAMPS /* diagnostic builds carry cycle stamps in the extra words */
@@ -1614,6 +1740,7 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
     if (expect >= 0 && xw[kXObs] != expect) {
       set_err("sweep %d sampled %lld observations, expected %lld: the statistics are incomplete or summed twice",
               iter, xw[kXObs], expect);
+      unwind();
       return -1;
     }
     for (int k = 0; k < n; k++) wrapped |= tot[k] < 0;
@@ -1621,6 +1748,7 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
       set_err("sweep %d: the fixed-point z sums overflowed int64 (zexp = %d leaves 2^%d time units; censored paths "
               "ran far past the observed times): pass a smaller zexp",
               iter, zexp, 63 - zexp);
+      unwind();
       return -1;
     }
     /* observations that hit a cap (ARMS iterations, path length, MHRS
@@ -1639,6 +1767,7 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
       set_err("sweep %d: %lld UNIF observations need more than %d uniformisation steps or mu*y > %g (the largest "
               "exit rate times the largest observation); their paths would be wrong: rescale the data",
               iter, xw[kXUnifCap], kUnifMaxK, kUnifMaxLam);
+      unwind();
       return -1;
     }
 #endif

@@ -47,6 +47,62 @@ extern "C" hipError_t pht_launch_stats_out(unsigned long long *d_stats, unsigned
   return hipGetLastError();
 }
 
+/* The pipelined Gibbs loop's gate (gibbs_host.cpp, gibbs_run): the next
+ * sweep is enqueued while the current one runs, behind this one-workgroup
+ * kernel, which waits until the host has written that sweep's parameter
+ * block (host-pinned coherent memory) and released `want` in the gate word,
+ * then copies the block to the device.  Thread 0 polls the gate with
+ * system-scope acquire loads (vector loads: nothing here goes through the
+ * scalar cache); a gate not released within ~4 s ends the wait anyway and
+ * the ack word says so (the host then fails the run: the sweep ran on stale
+ * parameters).  ack = want after a good copy. */
+__global__ void __launch_bounds__(256) pht_gate_kernel(const unsigned *gate, unsigned want,
+                                                       const unsigned long long *src, unsigned long long *dst,
+                                                       int nwords, unsigned *ack) {
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(); /* 100 MHz */
+    int good = 0;
+    for (;;) {
+      if (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == want) {
+        good = 1;
+        break;
+      }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    ok = good;
+  }
+  __syncthreads();
+  if (ok) {
+    /* eight loads in flight per thread (one link round trip per 2,048 words,
+     * the whole block at n <= 16) */
+    for (int base = 0; base < nwords; base += 8 * 256) {
+      unsigned long long v[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const int k = base + q * 256 + (int)threadIdx.x;
+        v[q] = k < nwords ? __hip_atomic_load(&src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const int k = base + q * 256 + (int)threadIdx.x;
+        if (k < nwords) dst[k] = v[q];
+      }
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(ack, ok ? want : ~want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" hipError_t pht_launch_gate(const unsigned *gate_dev, unsigned want, const unsigned long long *src_dev,
+                                      unsigned long long *dst, int nwords, unsigned *ack_dev, hipStream_t st) {
+  if (!gate_dev || !src_dev || !dst || !ack_dev || nwords < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pht_gate_kernel, dim3(1), dim3(256), 0, st, gate_dev, want, src_dev, dst, nwords, ack_dev);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t pht_launch_sweep(const pht::SweepArgs *a, int method, int debug, hipStream_t st) {
   using namespace pht;
   if (a->n < 1 || a->n > kMaxN) return hipErrorInvalidValue;

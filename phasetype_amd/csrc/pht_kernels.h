@@ -105,6 +105,8 @@ struct ResidentArgs {
 extern "C" hipError_t pht_launch_resident_update(const pht::ResidentArgs *r, int iter, hipStream_t st);
 extern "C" hipError_t pht_launch_sweep(const pht::SweepArgs *a, int method, int debug, hipStream_t st);
 /* the statistics block -> host-pinned memory + flag = seq, and zeroed (pht_dispatch.hip) */
+extern "C" hipError_t pht_launch_gate(const unsigned *gate_dev, unsigned want, const unsigned long long *src_dev,
+                                      unsigned long long *dst, int nwords, unsigned *ack_dev, hipStream_t st);
 extern "C" hipError_t pht_launch_stats_out(unsigned long long *d_stats, unsigned long long *h_out_dev,
                                            unsigned *flag_dev, unsigned seq, int sl, hipStream_t st);
 extern "C" hipError_t pht_launch_chains(const pht::SweepArgs *h, const pht::SweepArgs *d, int K, int method,

@@ -237,13 +237,10 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
    * (row j: cum[j (n + 1) + q]), so the scan reads a sum and a successor
    * with no dependent load and no addition (the same state every time) */
   /* (round 0 only: in the later rounds the sums' loads cost 4 VGPRs, 7 -> 6
-   * waves per SIMD at n = 10, and the round ran slower, cfg4 MHRS +3.4 %
-   * against -3.0 % with round 0 alone; profiles/r06/mhrs_cum/) */
-#ifdef PHT_MHRS_CUM_ALL
-  const bool usecum = mhrs_cum_bytes(n) > 0;
-#else
+   * waves per SIMD at n = 10, and the rounds ran slower, cfg4 MHRS +3.4 %
+   * against -3.0 % with round 0 alone; held to 7 waves +1.4 %, the
+   * successor read only on a hit: neutral; profiles/r06/mhrs_cum/) */
   const bool usecum = mhrs_cum_bytes(n) > 0 && W == 1;
-#endif
   PHT_LDS double *cum = (PHT_LDS double *)((PHT_LDS unsigned char *)cursor + 16);
   if (usecum) {
     if ((int)threadIdx.x < n) {
@@ -496,14 +493,9 @@ __device__ __forceinline__ void mhrs_search_body(const SweepArgs &a, uint32_t A0
 #endif
 }
 
-#ifdef PHT_MHRS_W7
-#define PHT_MHRS_WAVES __attribute__((amdgpu_waves_per_eu(7)))
-#else
-#define PHT_MHRS_WAVES
-#endif
 template <int NT, int W, int K>
-__global__ void __launch_bounds__(kBlock) PHT_MHRS_WAVES mhrs_search(SweepArgs a, uint32_t A0, const uint32_t *qin,
-                                                                     const unsigned *cin) {
+__global__ void __launch_bounds__(kBlock) mhrs_search(SweepArgs a, uint32_t A0, const uint32_t *qin,
+                                                      const unsigned *cin) {
   mhrs_search_body<NT, W, K>(a, A0, qin, cin, blockIdx.x, gridDim.x);
 }
 
