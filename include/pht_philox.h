@@ -148,24 +148,27 @@ PHT_HD2 void pht_stream_topup(pht_stream *s) {
 }
 
 #if defined(__HIPCC__)
-/* pht_stream_topup with the block's ten rounds unrolled (the same words):
- * for a kernel whose unit keeps the loop elsewhere (the MHRS search at
- * n = 15, PHT_MHRS_PHILOX_UNROLL) */
+/* the block with its ten rounds unrolled (the same words), and
+ * pht_stream_topup on it: for one kernel of a unit that keeps the loop
+ * elsewhere (PHT_MHRS_PHILOX_UNROLL etc., phasetype_amd/build.py) */
+__device__ __forceinline__ pht_u32x4 pht_philox4x32_10_unrolled(pht_u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    c = pht_philox_round(c, k0, k1);
+    k0 += 0x9E3779B9U;
+    k1 += 0xBB67AE85U;
+  }
+  return c;
+}
 __device__ __forceinline__ void pht_stream_topup_unrolled(pht_stream *s) {
   if (!s->nb) {
     pht_u32x4 c;
     c.v[0] = s->obs; c.v[1] = s->tag; c.v[2] = s->sweep; c.v[3] = s->blk++;
 #if defined(__HIP_DEVICE_COMPILE__)
-    uint32_t k0 = __builtin_amdgcn_readfirstlane(s->k0), k1 = __builtin_amdgcn_readfirstlane(s->k1);
+    c = pht_philox4x32_10_unrolled(c, __builtin_amdgcn_readfirstlane(s->k0), __builtin_amdgcn_readfirstlane(s->k1));
 #else
-    uint32_t k0 = s->k0, k1 = s->k1;
+    c = pht_philox4x32_10_unrolled(c, s->k0, s->k1);
 #endif
-#pragma unroll
-    for (int r = 0; r < 10; r++) {
-      c = pht_philox_round(c, k0, k1);
-      k0 += 0x9E3779B9U;
-      k1 += 0xBB67AE85U;
-    }
     s->b0 = c.v[0]; s->b1 = c.v[1]; s->b2 = c.v[2]; s->b3 = c.v[3];
     s->nb = 1;
   }

@@ -28,10 +28,12 @@ KERNEL_NTS = (10, 3, 5, 15, 20, 0)  # compile-time n of the kernels (0 = runtime
 UNIT_FLAGS = {10: ("-mllvm", "--amdgpu-schedule-metric-bias=0")}
 # Philox blocks with their ten rounds unrolled (the compiler keeps a loop of
 # two rounds otherwise; the same words): every kernel of the n = 5 and n = 20
-# units (cfg2 -4.1 %, cfg3 -1.4 % per sweep) and the MHRS search of the
-# n = 15 unit (cfg5 MHRS -1.4 %; the n = 15 ECS kernels lost 3.9 % with it);
-# neutral at n = 3 and n = 10, which keep the loop (profiles/r06/unroll/)
-UNIT_DEFINES = {5: ("PHT_PHILOX_UNROLL",), 20: ("PHT_PHILOX_UNROLL",), 15: ("PHT_MHRS_PHILOX_UNROLL",)}
+# units (cfg2 -4.1 %, cfg3 -1.4 % per sweep), the MHRS search of the n = 15
+# unit (cfg5 MHRS -1.4 %; every n = 15 kernel unrolled lost 3.9 % at cfg5 ECS)
+# and the ECS exact kernel's top-up at n = 10 and 15 (cfg4 -0.7 %, cfg5 ECS
+# -0.9 %; the censored kernel's: neutral) (profiles/r06/unroll/)
+UNIT_DEFINES = {5: ("PHT_PHILOX_UNROLL",), 20: ("PHT_PHILOX_UNROLL",),
+                10: ("PHT_ECS_PHILOX_UNROLL",), 15: ("PHT_MHRS_PHILOX_UNROLL", "PHT_ECS_PHILOX_UNROLL")}
 # (source, extra defines, extra device-compile flags) per object
 UNITS = [("pht_kernels_nt.hip", (f"PHT_NT={k}",) + UNIT_DEFINES.get(k, ()), UNIT_FLAGS.get(k, ()))
          for k in KERNEL_NTS] + [

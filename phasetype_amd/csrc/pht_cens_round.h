@@ -112,7 +112,11 @@ __device__ __forceinline__ void cens_round_body(const SweepArgs &a, unsigned blk
     if (!__any(have)) break;
     /* one converged Philox block per round (the stay test, the sojourn
      * and the next state draw 2-4 words outside ARMS) */
+#ifdef PHT_CENS_PHILOX_UNROLL
+    if (have) pht_stream_topup_unrolled(&ln.r);
+#else
     if (have) pht_stream_topup(&ln.r);
+#endif
     /* ---- one jump of every lane with a path */
     if (have && censored_jump(P, ln, env, sk, cl)) {
       const uint32_t nd = pht_stream_pos(&ln.r);

@@ -858,7 +858,11 @@ __device__ __forceinline__ void ecs_exact_body(const SweepArgs &a, unsigned blk,
       c.v[1] = cur ? ln.r.tag : 0u;
       c.v[2] = a.sweep;
       c.v[3] = cur ? ln.r.blk : 0u;
+#ifdef PHT_ECS_PHILOX_UNROLL
+      const pht_u32x4 w = pht_philox4x32_10_unrolled(c, a.k0, a.k1);
+#else
       const pht_u32x4 w = pht_philox4x32_10(c, a.k0, a.k1);
+#endif
       if (cur) {
         ln.r.b0 = w.v[0]; ln.r.b1 = w.v[1]; ln.r.b2 = w.v[2]; ln.r.b3 = w.v[3];
         ln.r.nb = 1;

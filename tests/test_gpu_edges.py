@@ -287,3 +287,41 @@ def test_published_statistics_equal_the_copy_path(gpu, monkeypatch, method):
     for a, b in zip(out["pub"], out["copy"]):
         assert np.array_equal(a, b)
     assert not np.array_equal(out["pub"][0], out["pub"][1])  # different sweeps, different draws
+
+
+@pytest.mark.parametrize("method", [2, 1, 4])
+def test_pipelined_loop_equals_serial(gpu, monkeypatch, method):
+    """The pipelined Gibbs loop (gibbs_host.cpp gibbs_run: sweep k + 1
+    enqueued behind pht_gate_kernel while sweep k runs) against the serial
+    loop (PHT_PIPELINE=0, read at context creation): the same chain, with the
+    censored range's concurrent stream (ECS) and the multi-kernel MHRS sweep.
+    Then a run that fails at its first sweep's check with the next sweep
+    already enqueued (a reduce that double-counts) must release that sweep and
+    leave the context usable: the next run equals a fresh context's chain."""
+    n = 5
+    T, nu, zeta, Cm, y, cen = _chain_setup(n, cf=0.3 if method != 4 else 0.0)
+    zexp = P.zexp_for(y)
+    res = {}
+    for mode in ("serial", "pipe"):
+        if mode == "serial":
+            monkeypatch.setenv("PHT_PIPELINE", "0")
+        else:
+            monkeypatch.delenv("PHT_PIPELINE", raising=False)
+        sw = P.Sweeper(n, method, 1)
+        sw.set_obs(y, cen)
+        sw.set_global_count(len(y))  # (checked with a reduce callback too)
+        P.set_seed(31)
+        res[mode] = sw.gibbs(8, method, nu, zeta, T, Cm, zexp).copy()
+        if mode == "pipe":
+            def twice(a):
+                a *= 2
+
+            P.set_seed(31)
+            with pytest.raises(P.PhaseTypeError, match="expected"):
+                sw.gibbs(8, method, nu, zeta, T, Cm, zexp, reduce=twice)
+            P.set_seed(31)
+            again = sw.gibbs(8, method, nu, zeta, T, Cm, zexp)
+            assert np.array_equal(again, res["serial"])
+        sw.close()
+    assert np.array_equal(res["serial"], res["pipe"])
+    assert np.all(np.isfinite(res["pipe"]))
