@@ -53,9 +53,10 @@ extern "C" hipError_t pht_launch_stats_out(unsigned long long *d_stats, unsigned
  * block (host-pinned coherent memory) and released `want` in the gate word,
  * then copies the block to the device.  Thread 0 polls the gate with
  * system-scope acquire loads (vector loads: nothing here goes through the
- * scalar cache); a gate not released within ~4 s ends the wait anyway and
+ * scalar cache); a gate not released within ~20 s ends the wait anyway and
  * the ack word says so (the host then fails the run: the sweep ran on stale
- * parameters).  ack = want after a good copy. */
+ * parameters), so no wave waits without bound.  ack = want after a good
+ * copy. */
 __global__ void __launch_bounds__(256) pht_gate_kernel(const unsigned *gate, unsigned want,
                                                        const unsigned long long *src, unsigned long long *dst,
                                                        int nwords, unsigned *ack) {
@@ -68,7 +69,7 @@ __global__ void __launch_bounds__(256) pht_gate_kernel(const unsigned *gate, uns
         good = 1;
         break;
       }
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) break;
       __builtin_amdgcn_s_sleep(2);
     }
     ok = good;
