@@ -1357,6 +1357,18 @@ static int ctx_enqueue(pht_ctx *c, uint32_t k0, uint32_t k1, uint32_t sweep, int
   return 0;
 }
 
+/* sweeps left in flight by an earlier call that failed: finish them and
+ * forget their records (their statistics are stale), so the next wait
+ * cannot take one of them for its own sweep */
+static void ctx_drain(pht_ctx *c) {
+  if (c->nin) {
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->nin = 0;
+    c->stats_zero = false;
+  }
+}
+
 /* release the pipelined sweep waiting at `gate`: its parameter block (pb
  * bytes) into the staging buffer, then the gate word (release store; the
  * gate kernel's acquire load orders its copy after it) */
@@ -1452,6 +1464,7 @@ extern "C" int pht_ctx_sweep(pht_ctx *c, const double *S, const double *s, uint3
   int info = build_params(c->n, S, s, c->method, pb);
   if (info < 0) return info;
   memcpy(c->h_params, pb.data(), pb.size());
+  ctx_drain(c);
   if (ctx_enqueue(c, k0, k1, sweep, zexp, false) || ctx_wait(c)) return -1;
   memcpy(stats_out, c->h_stats, sizeof(long long) * stats_len(c->n));
   return 0;
@@ -1466,6 +1479,7 @@ extern "C" int pht_ctx_sweep_debug(pht_ctx *c, const double *S, const double *s,
   int info = build_params(c->n, S, s, c->method, pb);
   if (info < 0) return info;
   memcpy(c->h_params, pb.data(), pb.size());
+  ctx_drain(c);
   if (ctx_enqueue(c, k0, k1, sweep, zexp, true) || ctx_wait(c)) return -1;
   memcpy(stats_out, c->h_stats, sizeof(long long) * stats_len(c->n));
   const long cnt = c->count;
@@ -1630,26 +1644,32 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
   double kms = 0.0;
   long ktimed = 0;
   long long flagged = 0;
-  /* Pipelined loop (one context, not a chains group, not UNIF, whose enqueue
+  /* Pipelined loop (contexts not in a chains group, not UNIF, whose enqueue
    * reads the parameters): sweep k + 1 is enqueued as soon as sweep k is,
-   * behind a gate kernel that waits for its parameters, so the launch work
-   * runs while sweep k does and only the Gamma update and the next
-   * parameter block stay between two sweeps (PHT_PIPELINE=0: off).  The
+   * behind a gate kernel per context that waits for its parameters, so the
+   * launch work runs while sweep k does and only the Gamma update and the
+   * next parameter block stay between two sweeps (PHT_PIPELINE=0: off).  The
    * draws are the same: sweep k + 1's parameters are those the update
    * produced from sweep k's statistics. */
-  pht_ctx *pc = ctxs.size() == 1 ? ctxs[0] : nullptr;
-  const bool pipe = pc && !pc->grp && pc->h_gate && pc->method != kMethodUNIF && !pc->ulaw && it > 2;
-  bool pending = false;
-  unsigned pgate = 0;
-  /* an early return with a gated sweep enqueued: release it (it runs on the
-   * last staged parameters) and drain the stream, so nothing waits on a gate */
+  for (pht_ctx *c : ctxs)
+    if (!c->grp) ctx_drain(c);
+  bool pipe = !ctxs.empty() && it > 2;
+  for (pht_ctx *c : ctxs) pipe = pipe && !c->grp && c->h_gate && c->method != kMethodUNIF && !c->ulaw;
+  bool pending = false;                        /* every context holds a gated sweep */
+  std::vector<unsigned> pgate(ctxs.size(), 0u); /* its gate (0: none enqueued) */
+  /* an early return with gated sweeps enqueued: release them (they run on
+   * the last staged parameters) and drain the streams, so nothing waits on
+   * a gate */
   auto unwind = [&]() {
-    if (pending) {
-      ctx_release(pc, pgate, nullptr, 0);
-      (void)hipStreamSynchronize(pc->stream);
-      pc->nin = 0;
-      pending = false;
+    for (size_t i = 0; i < ctxs.size(); i++) {
+      if (pgate[i]) {
+        ctx_release(ctxs[i], pgate[i], nullptr, 0);
+        (void)hipStreamSynchronize(ctxs[i]->stream);
+        ctxs[i]->nin = 0;
+        pgate[i] = 0u;
+      }
     }
+    pending = false;
   };
   int first_flagged = 0;
   /* every sweep must account for every observation of every shard: the
@@ -1690,8 +1710,11 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
     }
     const bool timed = want_time(iter);
     if (pending) {
-      memcpy(pc->h_params, pb.data(), pb.size());
-      ctx_release(pc, pgate, pb.data(), pb.size());
+      for (size_t i = 0; i < ctxs.size(); i++) {
+        memcpy(ctxs[i]->h_params, pb.data(), pb.size());
+        ctx_release(ctxs[i], pgate[i], pb.data(), pb.size());
+        pgate[i] = 0u;
+      }
       pending = false;
     } else {
       for (pht_ctx *c : ctxs) {
@@ -1704,14 +1727,16 @@ int gibbs_run(Rng &R, int it, int mhit, int method, int n, int m, const double *
       }
     }
     if (pipe && iter + 1 < it) {
-      if (++pc->gate_seq == 0u) pc->gate_seq = 1u;
-      pgate = pc->gate_seq;
-      if (ctx_enqueue(pc, k0, k1, (uint32_t)(iter + 1), zexp, false, want_time(iter + 1), pgate)) {
-        /* (a failed enqueue may have left the gate kernel in the stream) */
-        ctx_release(pc, pgate, nullptr, 0);
-        (void)hipStreamSynchronize(pc->stream);
-        pc->nin = 0;
-        return -1;
+      for (size_t i = 0; i < ctxs.size(); i++) {
+        pht_ctx *c = ctxs[i];
+        if (++c->gate_seq == 0u) c->gate_seq = 1u;
+        /* (recorded first: a failed enqueue may have left the gate kernel in
+         * the stream, and unwind releases it) */
+        pgate[i] = c->gate_seq;
+        if (ctx_enqueue(c, k0, k1, (uint32_t)(iter + 1), zexp, false, want_time(iter + 1), pgate[i])) {
+          unwind();
+          return -1;
+        }
       }
       pending = true;
     }
